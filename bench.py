@@ -1,0 +1,218 @@
+"""Benchmark: LoRa demod hot path (dechirp -> 2^SF FFT -> argmax) on MI355X.
+
+One step = one lora_demod_batch over this rank's batch of frames already resident in
+HBM: LEGACY lora_demodulate semantics with the fused caller-side dechirp
+(e2e_chain_test.cpp:85-101): normalisation, 2-symbol CFO/timing estimate, per-symbol
+CFO rotation, FFT, argmax, sync word.  Inputs are generated on the device by the
+bit-exact GPU modulator (lora_mod_batch), random symbols from a fixed seed.
+
+Headline workload (BASELINE.json configs[1]): SF7 BW125 osr 1, 1,000,000 data symbols
+= 15,625 frames x (2 sync + 64 data) per GPU.  The SF12 configuration (configs[2]) is
+measured in the same run and reported under "extra".  Multi-GPU: one process per GPU,
+frames sharded (no collective on the data path), weak scaling; value = data symbols of
+all ranks / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "lora-sdr-lightweight-standalone-library-_amd"))
+sys.path.insert(0, REPO)
+
+import lora_phy_amd as amd  # noqa: E402
+from lora_phy_amd import _capi  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+METRIC = "Msymbols/s dechirp+FFT+argmax @ SF7 & SF12, 1/2/4/8 GPU; % HBM roofline"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        import torch.distributed as dist
+
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, dist.get_rank(), world
+    torch.cuda.set_device(0)
+    return None, 0, 1
+
+
+def make_input(sf, frames, data_syms, seed, device, snr_db=None):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    syms = torch.randint(0, 1 << sf, (frames, data_syms), generator=g, dtype=torch.int32)
+    iq = amd.modulate(syms.to(device), sf, 1, 125000, 1.0, 0x12)
+    if snr_db is not None:
+        sigma = 10.0 ** (-snr_db / 20.0) / np.sqrt(2.0)
+        gn = torch.Generator(device=device).manual_seed(seed + 1)
+        noise = torch.randn(iq.shape + (2,), generator=gn, device=device) * sigma
+        iq = iq + torch.view_as_complex(noise)
+    return syms, iq
+
+
+def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=None):
+    N = 1 << sf
+    syms, iq = make_input(sf, frames, data_syms, 20251015 + rank, device, snr_db)
+    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device)
+    out = None
+    for _ in range(warmup):
+        out = plan.run(iq, out)
+    torch.cuda.synchronize(device)
+    lib = _capi.lib()
+    _capi.check(lib.lora_demod_profile_enable(plan._h, steps))
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = plan.run(iq, out)
+    torch.cuda.synchronize(device)
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    import ctypes as C
+
+    stage = (C.c_float * 3)()
+    calls = C.c_int()
+    _capi.check(lib.lora_demod_profile_read(plan._h, stage, C.byref(calls)))
+    lib.lora_demod_profile_enable(plan._h, 0)
+    stage_ms = [stage[k] / max(calls.value, 1) for k in range(3)]
+    t = torch.tensor([wall], dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    ok = bool(torch.equal(out.symbols.to(torch.int32).cpu(), syms)) if snr_db is None else None
+    total_syms = data_syms + 2
+    ms_step = wall * 1e3 / steps
+    B_sym = 8 * N + 2
+    # Dominant kernel = stage 2 (k_demod: every non-sync symbol).  Algorithmic bytes
+    # per launch = its symbols x (8*N*osr IQ read + 2 B index write).
+    demod_bytes = frames * data_syms * B_sym
+    dom_gbs = demod_bytes / (stage_ms[2] * 1e-3) / 1e9
+    pipe_bytes = frames * (total_syms * B_sym + 9)
+    return {
+        "sf": sf, "frames": frames, "data_symbols": frames * data_syms, "iq_bytes": iq.numel() * 8,
+        "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ok,
+        "msym_s_data": frames * data_syms / (ms_step * 1e-3) / 1e6,
+        "msym_s_all": frames * total_syms / (ms_step * 1e-3) / 1e6,
+        "dominant_kernel": "k_demod", "dominant_gbs": dom_gbs,
+        "dominant_bytes_per_launch": demod_bytes,
+        "pipeline_gbs": pipe_bytes / (ms_step * 1e-3) / 1e9,
+        "iq_host": None, "plan": plan, "iq": iq,
+    }
+
+
+def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=20.0):
+    from oracle.pyoracle import Oracle
+
+    O = Oracle()
+    F = min(iq_dev.shape[0], max_frames)
+    x = iq_dev[:F].cpu().numpy()
+    t0 = time.perf_counter()
+    done = 0
+    while True:
+        O.demod_frames(x, sf, 1, False, dechirp=True, threads=threads)
+        done += F
+        if time.perf_counter() - t0 > time_budget_s / 4 or done >= 4 * F:
+            break
+    dt = time.perf_counter() - t0
+    rate = done * data_syms / dt / 1e6
+    return {"value": rate, "unit": "Msymbols/s", "cores": threads, "kind": "port",
+            "sample": f"{done} frames (SF{sf}, {data_syms}+2 symbols each, dechirp+lora_demodulate "
+                      f"restatement oracle/lora_oracle.cpp, {threads} threads, {dt:.2f} s)"}
+
+
+def load_pmc(workload):
+    p = os.path.join(REPO, "profiles", "pmc_summary.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(workload, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=15625)
+    ap.add_argument("--data-symbols", type=int, default=64)
+    ap.add_argument("--sf12-frames", type=int, default=15625)
+    ap.add_argument("--no-sf12", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    args = ap.parse_args()
+
+    dist, rank, world = dist_setup(args.gpus)
+    device = torch.device("cuda", torch.cuda.current_device())
+    r7 = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, rank, dist, device)
+    extra = {}
+    if not args.no_sf12:
+        r12 = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2),
+                         args.warmup, rank, dist, device)
+        extra["sf12"] = {k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host")}
+        extra["sf12"]["value_all_ranks_msym_s"] = r12["msym_s_data"] * world
+        extra["sf12"]["roofline_frac"] = r12["dominant_gbs"] / HBM_PEAK_GBS
+        del r12
+        torch.cuda.empty_cache()
+    cpu = None
+    if rank == 0 and not args.no_cpu and world == 1:
+        try:
+            cpu = cpu_baseline(7, r7["iq"], args.data_symbols, 4000, args.cpu_threads)
+        except Exception as e:  # the CPU leg must not kill the GPU measurement
+            log("cpu baseline failed:", e)
+    if rank == 0:
+        workload = (f"SF7 BW125 osr1 LEGACY lora_demodulate + fused dechirp, {args.frames} frames x "
+                    f"(2 sync + {args.data_symbols} data) symbols per GPU, noiseless")
+        line = {
+            "metric": METRIC,
+            "value": r7["msym_s_data"] * world,
+            "unit": "Msymbols/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": r7["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (GPU lora_modulate of seeded random symbols, amplitude 1, no noise)",
+            "config": {"workload": workload, "sf": 7, "bw_hz": 125000, "osr": 1,
+                       "frames_per_gpu": args.frames, "data_symbols_per_frame": args.data_symbols,
+                       "parallelism": f"frames sharded x{world}, no collective",
+                       "symbols_ok": r7["symbols_ok"], "stage_ms": r7["stage_ms"],
+                       "msym_s_all_symbols": r7["msym_s_all"] * world,
+                       "pipeline_gbs_per_gpu": r7["pipeline_gbs"]},
+            "roofline": {"bound": "hbm", "kernel": r7["dominant_kernel"],
+                         "achieved": r7["dominant_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": r7["dominant_gbs"] / HBM_PEAK_GBS,
+                         "bytes_per_launch": r7["dominant_bytes_per_launch"],
+                         "traffic": load_pmc("sf7")},
+            "cpu_baseline": cpu,
+            "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,868 @@
+// lora_capi.hip — MI355X (gfx950) LoRa demodulator/modulator behind the C-ABI of
+// include/lora_mi355x.h.
+//
+// Demodulation of F frames is three launches on one stream (generic path, any SF
+// 2..12, any osr, any frame length):
+//   k_frame_max  LEGACY only: per-frame max(|I|,|Q|) of the (dechirped) samples,
+//                LoRaDemod.cpp:59-67, reduced with one atomicMax per workgroup.
+//   k_estimate   one workgroup per frame: the 2-symbol x osr-phase offset estimate
+//                (LoRaDemod.cpp:79-135 / phy.cpp:78-145) and the two sync symbols,
+//                leaving cfo / t_off / rate / scale in the workspace.
+//   k_demod      G = max(1, 1024/N) symbols per workgroup: (dechirp) -> (scale) ->
+//                CFO rotation (glibc-faithful sincosf) -> (window) -> LDS radix-4/2
+//                DIT FFT with kissfft's butterflies -> lowest-index argmax |X|^2
+//                (LoRaDemod.cpp:141-174, LoRaDetector.hpp:39-58).
+// A fused single-pass kernel for short frames lives in lora_fused.hip.
+//
+// All fp32 arithmetic follows the reference's operation order without contraction
+// (compiled with -ffp-contract=off, see lora_device.h), so outputs are bit-identical
+// to the reference's x86-64 build on the same inputs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lora_mi355x.h"
+#include "lora_device.h"
+
+#pragma clang fp contract(off)
+
+using lora::cf;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return set_error(LORA_EIO, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+  } while (0)
+
+const float PI_F = float(M_PI);
+
+// ---------------------------------------------------------------------------------
+// Host-side table generation (runs once per plan, on the host, with the reference's
+// exact formulas and the host libm, so the device sees the reference's constants).
+// ---------------------------------------------------------------------------------
+
+// ChirpGenerator.hpp:105-132 (genChirp), float recurrence, std::polar -> sincosf.
+void host_gen_chirp(std::complex<float>* out, int N, int osr, int NN, float f0, bool down,
+                    float ampl, float& phase, float bw_scale) {
+  const float fMin = -M_PI * bw_scale / osr;
+  const float fMax = M_PI * bw_scale / osr;
+  const float fStep = (2 * M_PI * bw_scale) / (N * osr * osr);
+  float f = fMin + f0;
+  for (int i = 0; i < NN; i++) {
+    f += fStep;
+    if (f > fMax) f -= (fMax - fMin);
+    if (down)
+      phase -= f;
+    else
+      phase += f;
+    float s, c;
+    sincosf(phase, &s, &c);
+    out[i] = std::complex<float>(ampl * c, ampl * s);
+  }
+  phase -= std::floor(phase / (2 * M_PI)) * 2 * M_PI;
+}
+
+// kissfft.hh:81-97: radix plan; only 4/2 radices occur for powers of two.
+std::vector<int> fft_radices(int nfft) {
+  std::vector<int> r;
+  int n = nfft, p = 4;
+  do {
+    while (n % p) {
+      p = (p == 4) ? 2 : (p == 2) ? 3 : p + 2;
+      if (p * p > n) p = n;
+    }
+    n /= p;
+    r.push_back(p);
+  } while (n > 1);
+  return r;
+}
+
+// Leaf order of kf_work (kissfft.hh:106-131): out position -> input index.
+void leaf_order(const std::vector<int>& radix, int stage, int out_pos, int in_idx, int fstride,
+                int len, std::vector<uint16_t>& rev) {
+  const int p = radix[stage];
+  const int m = len / p;
+  if (m == 1) {
+    for (int j = 0; j < p; ++j) rev[in_idx + j * fstride] = (uint16_t)(out_pos + j);
+    return;
+  }
+  for (int q = 0; q < p; ++q)
+    leaf_order(radix, stage + 1, out_pos + q * m, in_idx + q * fstride, fstride * p, m, rev);
+}
+
+float bw_scale_of(unsigned bw_hz) { return static_cast<float>(bw_hz) / 125000.0f; }  // phy.hpp:47-49
+
+bool bw_ok(unsigned bw) { return bw == 125000 || bw == 250000 || bw == 500000; }
+
+// ---------------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------------
+
+// Load sample j of a frame after the LEGACY caller-side dechirp and the
+// normalisation of LoRaDemod.cpp:68-77 (z = y * (1/max) when max > 1).
+__device__ __forceinline__ cf load_legacy(const cf* __restrict__ x, int64_t j,
+                                          const cf* __restrict__ down, int step, int dechirp,
+                                          int scaled, float scale) {
+  cf v = x[j];
+  if (dechirp) v = lora::cmul(v, down[j % step]);
+  if (scaled) v = lora::cscale(v, scale);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) k_frame_max(const cf* __restrict__ iq, int64_t frame_len,
+                                                   int64_t frame_stride, int bpf, int chunk,
+                                                   const cf* __restrict__ down, int step,
+                                                   int dechirp, uint32_t* __restrict__ maxbits) {
+  const int64_t f = blockIdx.x / bpf;
+  const int64_t c = blockIdx.x % bpf;
+  const cf* x = iq + f * frame_stride;
+  const int64_t j0 = c * (int64_t)chunk;
+  const int64_t j1 = min(j0 + (int64_t)chunk, frame_len);
+  float m = 0.0f;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+    const cf v = load_legacy(x, j, down, step, dechirp, 0, 1.0f);
+    m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+  }
+  for (int s = 32; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s, 64));
+  __shared__ float wmax[4];
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = wmax[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = fmaxf(r, wmax[w]);
+    if (r > 0.0f) atomicMax(&maxbits[f], __float_as_uint(r));
+  }
+}
+
+struct KArgs {
+  const cf* iq;
+  int64_t frame_len, frame_stride;
+  int sf, N, osr, step, total, have_sync, mode, dechirp, hann;
+  float power_scale;
+  const cf* tw;
+  const uint16_t* rev;
+  const float* win;
+  const cf* down;   // legacy dechirp table, `step` entries
+  const cf* down1;  // API per-symbol down-chirp, N entries
+  const uint32_t* maxbits;
+  lora::FrameParams* fp;
+  uint16_t* syms;
+  int64_t sym_stride;
+  uint8_t* sync;
+  float* cfo;
+  float* toff;
+  float* max_amp;
+  int est_only;  // lora_estimate_offsets_batch: all symbols, raw samples, outputs only
+};
+
+// Point i of symbol s of frame f, rotated/windowed, as fed to the detector
+// (LoRaDemod.cpp:142-162; phy.cpp:205-225 for API mode).
+__device__ __forceinline__ cf symbol_point(const KArgs& a, const cf* __restrict__ x,
+                                           const lora::FrameParams& p, int s, int i) {
+  int64_t base = (int64_t)s * a.step;
+  if (p.t_off > 0) {
+    if (base + p.t_off + a.step <= a.frame_len) base += p.t_off;
+  } else if (p.t_off < 0) {
+    const int64_t off = -(int64_t)p.t_off;
+    if (off <= base) base -= off;
+  }
+  const float start = p.rate * ((float)((uint32_t)s * (uint32_t)a.N) +
+                                (float)p.t_off / (float)a.osr);
+  const float ph = start + p.rate * (float)i;
+  float sn, cs;
+  lm_sincosf(ph, &sn, &cs);
+  const int64_t j = base + (int64_t)i * a.osr;
+  cf v;
+  if (a.mode == LORA_MODE_API) {
+    v = lora::cmul(lora::cmul(x[j], a.down1[i]), cf{cs, sn});
+  } else {
+    v = lora::cmul(load_legacy(x, j, a.down, a.step, a.dechirp, p.scaled, p.scale), cf{cs, sn});
+  }
+  if (a.hann) v = lora::cscale(v, a.win[i]);
+  return v;
+}
+
+// Workgroup argmax of one N-point spectrum in LDS (natural order).  Returns the
+// key to every thread.
+__device__ __forceinline__ uint64_t wg_argmax(const cf* A, int N, uint64_t* red) {
+  uint64_t k = 0;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) k = lora::umax64(k, lora::argmax_key(A[i], i));
+  k = lora::group_max(k, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = k;
+  __syncthreads();
+  uint64_t r = red[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = lora::umax64(r, red[w]);
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(256) k_estimate(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cf* A = reinterpret_cast<cf*>(smem);
+  __shared__ uint64_t red[4];
+  __shared__ lora::FrameParams sp;
+  __shared__ uint16_t sw[2];
+  const int f = blockIdx.x;
+  const cf* x = a.iq + (int64_t)f * a.frame_stride;
+  const int N = a.N;
+
+  // Normalisation decision (LoRaDemod.cpp:68-77); API mode never normalises.
+  float scale = 1.0f;
+  int scaled = 0;
+  float maxv = 0.0f;
+  if (a.mode == LORA_MODE_LEGACY && !a.est_only) {
+    maxv = __uint_as_float(a.maxbits[f]);
+    if (maxv > 1.0f) {
+      scaled = 1;
+      scale = 1.0f / maxv;
+    }
+  }
+  const bool raw = a.mode == LORA_MODE_API || a.est_only;
+  const int est = a.est_only ? a.total : (a.mode == LORA_MODE_API) ? 2 : min(a.total, 2);
+  const bool tie_rule = a.mode == LORA_MODE_LEGACY && !a.est_only;
+
+  // Scalar estimator state lives in thread 0.
+  float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
+  bool have_prev = false;
+  unsigned sum_t = 0;
+  for (int s = 0; s < est; ++s) {
+    float best_p = -1e30f, best_fi = 0.0f;
+    uint32_t best_idx = 0;
+    unsigned best_t = 0;
+    cf best_bin = {0.0f, 0.0f};
+    for (int t = 0; t < a.osr; ++t) {
+      for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const int64_t j = (int64_t)s * a.step + t + (int64_t)i * a.osr;
+        cf v = raw ? x[j] : load_legacy(x, j, a.down, a.step, a.dechirp, scaled, scale);
+        if (a.hann) v = lora::cscale(v, a.win[i]);
+        A[a.rev[i]] = v;
+      }
+      __syncthreads();
+      lora::fft_lds(A, a.sf, 1, a.tw, threadIdx.x, blockDim.x);
+      const uint64_t key = wg_argmax(A, N, red);
+      if (threadIdx.x == 0) {
+        const uint32_t idx = lora::key_index(key);
+        const float mv = lora::key_value(key);
+        float p, fi;
+        lora::detect_tail(mv, A[idx > 0 ? idx - 1 : N - 1], A[idx < (uint32_t)N - 1 ? idx + 1 : 0],
+                          a.power_scale, &p, &fi);
+        if (p > best_p || (tie_rule && p == best_p && idx < best_idx)) {
+          best_p = p;
+          best_idx = idx;
+          best_fi = fi;
+          best_t = t;
+          best_bin = A[idx];
+        }
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      sum_t += best_t;
+      sum_index += (float)best_idx + best_fi;
+      const float phase = lm_atan2f(best_bin.im, best_bin.re);
+      if (have_prev) {
+        float d = phase - prev_phase;
+        while (d > PI_F) d -= 2.0f * PI_F;
+        while (d < -PI_F) d += 2.0f * PI_F;
+        phase_diff += d;
+      }
+      prev_phase = phase;
+      have_prev = true;
+    }
+  }
+  if (a.est_only) {  // phy.cpp:87: no whole symbol -> metrics untouched
+    if (threadIdx.x == 0 && est > 0) {
+      const float avg_index = sum_index / (float)est;
+      const float cfo_coarse = avg_index / (float)N;
+      float cfo_fine = 0.0f;
+      if (est > 1) cfo_fine = (phase_diff / (float)(est - 1)) / (2.0f * PI_F * (float)N);
+      const float frac = avg_index - floorf(avg_index + 0.5f);
+      const float avg_t = (float)sum_t / (float)est;
+      if (a.cfo) a.cfo[f] = cfo_coarse + cfo_fine;
+      if (a.toff) a.toff[f] = avg_t - frac * (float)N * (float)a.osr;
+    }
+    return;
+  }
+  if (threadIdx.x == 0) {
+    const float avg_index = sum_index / (float)est;
+    const float cfo_coarse = avg_index / (float)N;
+    float cfo_fine = 0.0f;
+    if (est > 1) cfo_fine = (phase_diff / (float)(est - 1)) / (2.0f * PI_F * (float)N);
+    const float cfo = cfo_coarse + cfo_fine;
+    const float frac = avg_index - floorf(avg_index + 0.5f);
+    const float avg_t = (float)sum_t / (float)est;
+    const float toff = avg_t - frac * (float)N * (float)a.osr;
+    lora::FrameParams p;
+    p.cfo = cfo;
+    p.toff = toff;
+    p.t_off = (int)roundf(toff);
+    p.rate = -2.0f * PI_F * cfo / (float)N;
+    p.scale = scale;
+    p.scaled = scaled;
+    p.pad0 = p.pad1 = 0;
+    sp = p;
+    a.fp[f] = p;
+    if (a.cfo) a.cfo[f] = cfo;
+    if (a.toff) a.toff[f] = toff;
+    if (a.max_amp) a.max_amp[f] = maxv;
+  }
+  __syncthreads();
+
+  // Sync symbols 0 and 1 (LoRaDemod.cpp:165-168, 177-192; phy.cpp:228-237).
+  if (a.have_sync) {
+    const lora::FrameParams p = sp;
+    for (int s = 0; s < 2; ++s) {
+      for (int i = threadIdx.x; i < N; i += blockDim.x) A[a.rev[i]] = symbol_point(a, x, p, s, i);
+      __syncthreads();
+      lora::fft_lds(A, a.sf, 1, a.tw, threadIdx.x, blockDim.x);
+      const uint64_t key = wg_argmax(A, N, red);
+      if (threadIdx.x == 0) sw[s] = (uint16_t)lora::key_index(key);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0 && a.sync) {
+      const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
+      a.sync[f] = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
+    }
+  } else if (threadIdx.x == 0 && a.sync) {
+    a.sync[f] = 0;
+  }
+}
+
+// G symbols per workgroup; work item w -> (frame, symbol) over the symbols that are
+// not sync symbols.
+__global__ void __launch_bounds__(256) k_demod(KArgs a, int G, int s0, int64_t work) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cf* A = reinterpret_cast<cf*>(smem);
+  const int N = a.N;
+  const int per = a.total - s0;
+  const int64_t w0 = (int64_t)blockIdx.x * G;
+  const int P = G * N;
+  for (int q = threadIdx.x; q < P; q += blockDim.x) {
+    const int g = q >> a.sf;
+    const int i = q & (N - 1);
+    const int64_t w = w0 + g;
+    cf v = {0.0f, 0.0f};
+    if (w < work) {
+      const int64_t f = w / per;
+      const int s = s0 + (int)(w - f * per);
+      const lora::FrameParams p = a.fp[f];
+      v = symbol_point(a, a.iq + f * a.frame_stride, p, s, i);
+    }
+    A[g * N + a.rev[i]] = v;
+  }
+  __syncthreads();
+  lora::fft_lds(A, a.sf, G, a.tw, threadIdx.x, blockDim.x);
+  // Argmax: T = 256/G threads per symbol.
+  const int T = blockDim.x / G;
+  const int g = threadIdx.x / T;
+  const int lt = threadIdx.x % T;
+  uint64_t k = 0;
+  for (int i = lt; i < N; i += T) k = lora::umax64(k, lora::argmax_key(A[g * N + i], i));
+  __shared__ uint64_t red[4];
+  if (T <= 64) {
+    k = lora::group_max(k, T);
+  } else {
+    k = lora::group_max(k, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = k;
+    __syncthreads();
+    const int wpg = T >> 6;
+    const int wb = (threadIdx.x >> 6) / wpg * wpg;
+    k = red[wb];
+    for (int u = 1; u < wpg; ++u) k = lora::umax64(k, red[wb + u]);
+  }
+  if (lt == 0) {
+    const int64_t w = w0 + g;
+    if (w < work && a.syms) {
+      const int64_t f = w / per;
+      const int s = (int)(w - f * per);
+      a.syms[f * a.sym_stride + s] = (uint16_t)lora::key_index(k);
+    }
+  }
+}
+
+// phy.cpp:147-176 (compensate_offsets), out of place: rotation by rate*n first,
+// then the integer shift with zero fill.
+__global__ void __launch_bounds__(256) k_compensate(const cf* __restrict__ in, cf* __restrict__ out,
+                                                    int64_t frame_len, int64_t frame_stride,
+                                                    int64_t frames, float Nosr,
+                                                    const float* __restrict__ cfo,
+                                                    const float* __restrict__ toff) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= frames * frame_len) return;
+  const int64_t f = gid / frame_len;
+  const int64_t n = gid - f * frame_len;
+  const float rate = -2.0f * PI_F * cfo[f] / Nosr;
+  const int offset = (int)roundf(toff[f]);
+  int64_t src = n;
+  bool zero = false;
+  if (offset > 0 && (int64_t)offset < frame_len) {
+    src = n - offset;
+    zero = src < 0;
+  } else if (offset < 0 && -(int64_t)offset < frame_len) {
+    src = n - offset;
+    zero = src >= frame_len;
+  }
+  cf v = {0.0f, 0.0f};
+  if (!zero) {
+    const float ph = rate * (float)(uint64_t)src;
+    float sn, cs;
+    lm_sincosf(ph, &sn, &cs);
+    v = lora::cmul(in[f * frame_stride + src], cf{cs, sn});
+  }
+  out[f * frame_stride + n] = v;
+}
+
+// ---------------------------------------------------------------------------------
+// Modulator (LoRaMod.cpp:8-43): chirp start phases by one lane per frame (the fp32
+// phase recurrence is sequential), then one lane per chirp emits its samples.
+// ---------------------------------------------------------------------------------
+struct ModArgs {
+  int N, osr, step, nchirp;
+  float fMin, fMax, fStep, ampl, bw_scale;
+  uint16_t sw0, sw1;
+  const uint16_t* syms;
+  int64_t sym_count;
+  cf* iq;
+  int64_t frames;
+};
+
+__device__ __forceinline__ float chirp_f0(const ModArgs& a, int64_t frame, int c) {
+  const unsigned v = c == 0 ? a.sw0 : c == 1 ? a.sw1 : a.syms[frame * a.sym_count + (c - 2)];
+  return (2.0f * PI_F * (float)(int)v * a.bw_scale) / ((float)a.N * (float)a.osr);
+}
+
+__global__ void k_mod_phase(ModArgs a) {
+  const int64_t fr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (fr >= a.frames) return;
+  cf* out = a.iq + fr * (int64_t)a.nchirp * a.step;
+  float phase = 0.0f;
+  const float span = a.fMax - a.fMin;
+  for (int c = 0; c < a.nchirp; ++c) {
+    out[(int64_t)c * a.step].re = phase;  // start phase, consumed by k_mod_samples
+    float f = a.fMin + chirp_f0(a, fr, c);
+    for (int i = 0; i < a.step; ++i) {
+      f += a.fStep;
+      if (f > a.fMax) f -= span;
+      phase += f;
+    }
+    phase = (float)((double)phase - floor((double)phase / (2 * M_PI)) * 2 * M_PI);
+  }
+}
+
+__global__ void k_mod_samples(ModArgs a) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= a.frames * a.nchirp) return;
+  const int64_t fr = w / a.nchirp;
+  const int c = (int)(w - fr * a.nchirp);
+  cf* out = a.iq + w * a.step;
+  float phase = out[0].re;
+  float f = a.fMin + chirp_f0(a, fr, c);
+  const float span = a.fMax - a.fMin;
+  for (int i = 0; i < a.step; ++i) {
+    f += a.fStep;
+    if (f > a.fMax) f -= span;
+    phase += f;
+    float s, co;
+    lm_sincosf(phase, &s, &co);
+    out[i] = cf{a.ampl * co, a.ampl * s};
+  }
+}
+
+}  // namespace
+
+// ===================================================================================
+// Plan
+// ===================================================================================
+struct lora_demod_plan {
+  lora_demod_params prm;
+  int N, step;
+  float power_scale;
+  void* dev_tables;  // one allocation: tw | down | down1 | win | rev
+  cf* tw;
+  cf* down;
+  cf* down1;
+  float* win;
+  uint16_t* rev;
+  // measurement hooks (lora_demod_profile_enable)
+  std::vector<hipEvent_t> prof_ev;  // 4 per recorded call
+  int prof_max = 0, prof_calls = 0;
+};
+
+namespace {
+void prof_record(lora_demod_plan* plan, int stage, hipStream_t st) {
+  if (plan->prof_calls >= plan->prof_max) return;
+  hipEventRecord(plan->prof_ev[(size_t)plan->prof_calls * 4 + stage], st);
+}
+}  // namespace
+
+extern "C" {
+
+const char* lora_version(void) { return "lora_mi355x 0.1 (gfx950)"; }
+
+const char* lora_last_error(void) { return g_last_error.c_str(); }
+
+int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** out) {
+  if (!params || !out) return set_error(LORA_EINVAL, "null argument");
+  lora_demod_params p = *params;
+  if (p.sf < 2 || p.sf > 12) return set_error(LORA_EINVAL, "sf must be in 2..12");
+  if (p.osr == 0) p.osr = 1;  // phy.cpp:32
+  if (p.osr > 64) return set_error(LORA_EINVAL, "osr must be <= 64");
+  if (!bw_ok(p.bw_hz)) return set_error(LORA_EINVAL, "bw_hz must be 125000, 250000 or 500000");
+  if (p.window != LORA_WINDOW_NONE && p.window != LORA_WINDOW_HANN)
+    return set_error(LORA_EINVAL, "bad window");
+  if (p.mode != LORA_MODE_LEGACY && p.mode != LORA_MODE_API) return set_error(LORA_EINVAL, "bad mode");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (p.device < 0 || p.device >= ndev) return set_error(LORA_EINVAL, "bad device ordinal");
+
+  const int N = 1 << p.sf;
+  const int step = N * (int)p.osr;
+  const float bws = bw_scale_of(p.bw_hz);
+  // kissfft.hh:24-29 twiddles; LoRaDemod.cpp:17-25 window; genChirp down-chirps.
+  std::vector<std::complex<float>> tw(N), down(step), down1(N);
+  const float phinc = -2 * std::acos((float)-1) / N;
+  for (int i = 0; i < N; ++i) tw[i] = std::exp(std::complex<float>(0, i * phinc));
+  float ph = 0.0f;
+  host_gen_chirp(down.data(), N, (int)p.osr, step, 0.0f, true, 1.0f, ph, bws);
+  ph = 0.0f;
+  host_gen_chirp(down1.data(), N, 1, N, 0.0f, true, 1.0f, ph, bws);
+  std::vector<float> win(N);
+  for (int i = 0; i < N; ++i)
+    win[i] = p.window == LORA_WINDOW_HANN
+                 ? 0.5f - 0.5f * std::cos(2.0f * PI_F * static_cast<float>(i) /
+                                          (static_cast<float>(N) - 1.0f))
+                 : 1.0f;
+  std::vector<uint16_t> rev(N);
+  leaf_order(fft_radices(N), 0, 0, 0, 1, N, rev);
+  for (int r : fft_radices(N))
+    if (r != 2 && r != 4) return set_error(LORA_EINVAL, "unexpected FFT radix");
+
+  const size_t b_tw = sizeof(cf) * N, b_down = sizeof(cf) * step, b_down1 = sizeof(cf) * N,
+               b_win = sizeof(float) * N, b_rev = sizeof(uint16_t) * N;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t total = al(b_tw) + al(b_down) + al(b_down1) + al(b_win) + al(b_rev);
+
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  HIP_TRY(hipSetDevice(p.device));
+  void* mem = nullptr;
+  if (hipMalloc(&mem, total) != hipSuccess) {
+    hipSetDevice(prev);
+    return set_error(LORA_ENOMEM, "hipMalloc of plan tables failed");
+  }
+  unsigned char* b = static_cast<unsigned char*>(mem);
+  lora_demod_plan* plan = new lora_demod_plan();
+  plan->prm = p;
+  plan->N = N;
+  plan->step = step;
+  plan->power_scale = 20 * std::log10(static_cast<size_t>(N));  // LoRaDetector.hpp:29
+  plan->dev_tables = mem;
+  plan->tw = reinterpret_cast<cf*>(b);
+  b += al(b_tw);
+  plan->down = reinterpret_cast<cf*>(b);
+  b += al(b_down);
+  plan->down1 = reinterpret_cast<cf*>(b);
+  b += al(b_down1);
+  plan->win = reinterpret_cast<float*>(b);
+  b += al(b_win);
+  plan->rev = reinterpret_cast<uint16_t*>(b);
+  hipError_t e = hipMemcpy(plan->tw, tw.data(), b_tw, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(plan->down, down.data(), b_down, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(plan->down1, down1.data(), b_down1, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(plan->win, win.data(), b_win, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(plan->rev, rev.data(), b_rev, hipMemcpyHostToDevice);
+  hipSetDevice(prev);
+  if (e != hipSuccess) {
+    hipFree(mem);
+    delete plan;
+    return set_error(LORA_EIO, std::string("plan table upload: ") + hipGetErrorString(e));
+  }
+  *out = plan;
+  return LORA_OK;
+}
+
+int lora_demod_profile_enable(lora_demod_plan* plan, int max_calls) {
+  if (!plan || max_calls < 0) return set_error(LORA_EINVAL, "bad argument");
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  HIP_TRY(hipSetDevice(plan->prm.device));
+  for (hipEvent_t e : plan->prof_ev) hipEventDestroy(e);
+  plan->prof_ev.assign((size_t)max_calls * 4, nullptr);
+  for (auto& e : plan->prof_ev) HIP_TRY(hipEventCreate(&e));
+  plan->prof_max = max_calls;
+  plan->prof_calls = 0;
+  HIP_TRY(hipSetDevice(prev));
+  return LORA_OK;
+}
+
+int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls) {
+  if (!plan || !stage_ms || !calls) return set_error(LORA_EINVAL, "bad argument");
+  for (int k = 0; k < 3; ++k) stage_ms[k] = 0.0f;
+  *calls = plan->prof_calls;
+  if (plan->prof_calls == 0) return LORA_OK;
+  HIP_TRY(hipEventSynchronize(plan->prof_ev[(size_t)plan->prof_calls * 4 - 1]));
+  for (int c = 0; c < plan->prof_calls; ++c)
+    for (int k = 0; k < 3; ++k) {
+      float ms = 0.0f;
+      HIP_TRY(hipEventElapsedTime(&ms, plan->prof_ev[(size_t)c * 4 + k], plan->prof_ev[(size_t)c * 4 + k + 1]));
+      stage_ms[k] += ms;
+    }
+  return LORA_OK;
+}
+
+int lora_demod_plan_destroy(lora_demod_plan* plan) {
+  if (!plan) return LORA_OK;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(plan->prm.device);
+  for (hipEvent_t e : plan->prof_ev) hipEventDestroy(e);
+  hipFree(plan->dev_tables);
+  hipSetDevice(prev);
+  delete plan;
+  return LORA_OK;
+}
+
+int64_t lora_demod_symbols_per_frame(const lora_demod_plan* plan, int64_t frame_len) {
+  if (!plan || frame_len < 0) return set_error(LORA_EINVAL, "bad argument");
+  const int64_t total = frame_len / plan->step;
+  if (plan->prm.mode == LORA_MODE_API) {
+    if (frame_len % plan->step != 0)  // phy.cpp:186
+      return set_error(LORA_EINVAL, "API mode: frame_len must be a multiple of N*osr");
+    if (total < 2) return set_error(LORA_EINVAL, "API mode: frame needs >= 2 symbols");  // phy.cpp:188
+    return total - 2;
+  }
+  return total >= 2 ? total - 2 : total;  // LoRaDemod.cpp:194
+}
+
+size_t lora_demod_workspace_bytes(const lora_demod_plan* plan, int64_t frames) {
+  (void)plan;
+  if (frames <= 0) return 0;
+  const size_t mb = ((size_t)frames * sizeof(uint32_t) + 255) & ~size_t(255);
+  return mb + (size_t)frames * sizeof(lora::FrameParams);
+}
+
+int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames, int64_t frame_len,
+                         int64_t frame_stride, const lora_demod_outputs* out, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  if (!plan || !out) return set_error(LORA_EINVAL, "null argument");
+  if (frames < 0 || frame_len < 0 || frame_stride < frame_len)
+    return set_error(LORA_EINVAL, "bad frames / frame_len / frame_stride");
+  if (frame_len >= (int64_t(1) << 31)) return set_error(LORA_EINVAL, "frame_len must be < 2^31");
+  const int64_t nsym = lora_demod_symbols_per_frame(plan, frame_len);
+  if (nsym < 0) return nsym;
+  if (frames == 0) return nsym;
+  if (!iq) return set_error(LORA_EINVAL, "null iq");
+  if (out->symbols && out->sym_stride < nsym)
+    return set_error(LORA_ERANGE, "sym_stride smaller than symbols per frame");  // phy.cpp:190
+  const size_t need = lora_demod_workspace_bytes(plan, frames);
+  if (!workspace || workspace_bytes < need)
+    return set_error(LORA_ERANGE, "workspace too small");
+
+  const lora_demod_params& p = plan->prm;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  if (prev != p.device) HIP_TRY(hipSetDevice(p.device));
+
+  const int64_t total = frame_len / plan->step;
+  KArgs a;
+  a.iq = reinterpret_cast<const cf*>(iq);
+  a.frame_len = frame_len;
+  a.frame_stride = frame_stride;
+  a.sf = (int)p.sf;
+  a.N = plan->N;
+  a.osr = (int)p.osr;
+  a.step = plan->step;
+  a.total = (int)total;
+  a.mode = p.mode;
+  a.have_sync = (p.mode == LORA_MODE_API) ? 1 : (total >= 2 ? 1 : 0);
+  a.dechirp = (p.mode == LORA_MODE_LEGACY && p.dechirp) ? 1 : 0;
+  a.hann = p.window == LORA_WINDOW_HANN;
+  a.power_scale = plan->power_scale;
+  a.tw = plan->tw;
+  a.rev = plan->rev;
+  a.win = plan->win;
+  a.down = plan->down;
+  a.down1 = plan->down1;
+  unsigned char* wsb = static_cast<unsigned char*>(workspace);
+  uint32_t* maxbits = reinterpret_cast<uint32_t*>(wsb);
+  a.maxbits = maxbits;
+  a.fp = reinterpret_cast<lora::FrameParams*>(wsb + (((size_t)frames * 4 + 255) & ~size_t(255)));
+  a.syms = out->symbols;
+  a.sym_stride = out->sym_stride;
+  a.sync = out->sync;
+  a.cfo = out->cfo;
+  a.toff = out->time_offset;
+  a.max_amp = out->max_amp;
+  a.est_only = 0;
+
+  int rc = LORA_OK;
+  prof_record(plan, 0, st);
+  do {
+    if (p.mode == LORA_MODE_LEGACY) {
+      if (hipMemsetAsync(maxbits, 0, (size_t)frames * 4, st) != hipSuccess) {
+        rc = set_error(LORA_EIO, "hipMemsetAsync failed");
+        break;
+      }
+      if (frame_len > 0) {
+        const int chunk = 4096;
+        const int bpf = (int)((frame_len + chunk - 1) / chunk);
+        const int64_t grid = frames * bpf;
+        if (grid >= (int64_t(1) << 31)) {
+          rc = set_error(LORA_EINVAL, "batch too large");
+          break;
+        }
+        hipLaunchKernelGGL(k_frame_max, dim3((unsigned)grid), dim3(256), 0, st, a.iq, frame_len,
+                           frame_stride, bpf, chunk, a.down, a.step, a.dechirp, maxbits);
+      }
+    }
+    prof_record(plan, 1, st);
+    hipLaunchKernelGGL(k_estimate, dim3((unsigned)frames), dim3(256), sizeof(cf) * plan->N, st, a);
+    prof_record(plan, 2, st);
+    const int s0 = a.have_sync ? 2 : 0;
+    const int64_t per = total - s0;
+    const int64_t work = frames * per;
+    if (work > 0) {
+      const int G = std::max(1, 1024 / plan->N);
+      const int64_t grid = (work + G - 1) / G;
+      hipLaunchKernelGGL(k_demod, dim3((unsigned)grid), dim3(256), sizeof(cf) * G * plan->N, st, a,
+                         G, s0, work);
+    }
+    prof_record(plan, 3, st);
+    if (plan->prof_calls < plan->prof_max) ++plan->prof_calls;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) rc = set_error(LORA_EIO, std::string("kernel launch: ") + hipGetErrorString(e));
+  } while (0);
+  if (prev != p.device) hipSetDevice(prev);
+  return rc < 0 ? rc : nsym;
+}
+
+int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitude, uint8_t sync,
+                       const uint16_t* symbols, int64_t frames, int64_t sym_count, float* iq,
+                       int device, void* stream) {
+  if (sf < 2 || sf > 12) return set_error(LORA_EINVAL, "sf must be in 2..12");
+  if (osr == 0) osr = 1;
+  if (!bw_ok(bw_hz)) return set_error(LORA_EINVAL, "bad bw_hz");
+  if (frames < 0 || sym_count < 0) return set_error(LORA_EINVAL, "bad sizes");
+  const int N = 1 << sf;
+  const int step = N * (int)osr;
+  const int64_t per_frame = (sym_count + 2) * (int64_t)step;
+  if (frames == 0) return per_frame;
+  if (!iq || (sym_count > 0 && !symbols)) return set_error(LORA_EINVAL, "null buffer");
+  const float bws = bw_scale_of(bw_hz);
+  ModArgs a;
+  a.N = N;
+  a.osr = (int)osr;
+  a.step = step;
+  a.nchirp = (int)(sym_count + 2);
+  a.fMin = -M_PI * bws / osr;  // ChirpGenerator.hpp:107-109 (double -> float)
+  a.fMax = M_PI * bws / osr;
+  a.fStep = (2 * M_PI * bws) / (N * osr * osr);
+  a.ampl = std::max(-1.0f, std::min(1.0f, amplitude));  // LoRaMod.cpp:16
+  a.bw_scale = bws;
+  const unsigned shift = sf > 4 ? sf - 4 : 0;
+  a.sw0 = (uint16_t)((sync >> 4) << shift);
+  a.sw1 = (uint16_t)((sync & 0x0f) << shift);
+  a.syms = symbols;
+  a.sym_count = sym_count;
+  a.iq = reinterpret_cast<cf*>(iq);
+  a.frames = frames;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  if (prev != device) HIP_TRY(hipSetDevice(device));
+  hipLaunchKernelGGL(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, a);
+  const int64_t chirps = frames * a.nchirp;
+  hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((chirps + 63) / 64)), dim3(64), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (prev != device) hipSetDevice(prev);
+  if (e != hipSuccess) return set_error(LORA_EIO, std::string("mod launch: ") + hipGetErrorString(e));
+  return per_frame;
+}
+
+int64_t lora_estimate_offsets_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
+                                    int64_t frame_len, int64_t frame_stride, float* cfo,
+                                    float* time_offset, void* stream) {
+  if (!plan) return set_error(LORA_EINVAL, "null plan");
+  if (frames < 0 || frame_len < 0 || frame_stride < frame_len)
+    return set_error(LORA_EINVAL, "bad frames / frame_len / frame_stride");
+  if (frame_len >= (int64_t(1) << 31)) return set_error(LORA_EINVAL, "frame_len must be < 2^31");
+  const int64_t total = frame_len / plan->step;
+  if (frames == 0 || total == 0) return total;
+  if (!iq) return set_error(LORA_EINVAL, "null iq");
+  const lora_demod_params& p = plan->prm;
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  if (prev != p.device) HIP_TRY(hipSetDevice(p.device));
+  KArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.iq = reinterpret_cast<const cf*>(iq);
+  a.frame_len = frame_len;
+  a.frame_stride = frame_stride;
+  a.sf = (int)p.sf;
+  a.N = plan->N;
+  a.osr = (int)p.osr;
+  a.step = plan->step;
+  a.total = (int)total;
+  a.mode = LORA_MODE_API;
+  a.hann = p.window == LORA_WINDOW_HANN;
+  a.power_scale = plan->power_scale;
+  a.tw = plan->tw;
+  a.rev = plan->rev;
+  a.win = plan->win;
+  a.down = plan->down;
+  a.down1 = plan->down1;
+  a.cfo = cfo;
+  a.toff = time_offset;
+  a.est_only = 1;
+  hipLaunchKernelGGL(k_estimate, dim3((unsigned)frames), dim3(256), sizeof(cf) * plan->N,
+                     static_cast<hipStream_t>(stream), a);
+  hipError_t e = hipGetLastError();
+  if (prev != p.device) hipSetDevice(prev);
+  if (e != hipSuccess) return set_error(LORA_EIO, std::string("estimate launch: ") + hipGetErrorString(e));
+  return total;
+}
+
+int64_t lora_compensate_offsets_batch(unsigned sf, unsigned osr, const float* in, int64_t frames,
+                                      int64_t frame_len, int64_t frame_stride, const float* cfo,
+                                      const float* time_offset, int device, void* stream,
+                                      float* out) {
+  if (sf < 2 || sf > 12) return set_error(LORA_EINVAL, "sf must be in 2..12");
+  if (osr == 0) osr = 1;
+  if (frames < 0 || frame_len < 0 || frame_stride < frame_len)
+    return set_error(LORA_EINVAL, "bad frames / frame_len / frame_stride");
+  if (frames == 0 || frame_len == 0) return frame_len;
+  if (!in || !out || !cfo || !time_offset) return set_error(LORA_EINVAL, "null buffer");
+  if (in == out) return set_error(LORA_EINVAL, "in and out must not overlap");
+  const float Nosr = static_cast<float>(1u << sf) * static_cast<float>(osr);  // phy.cpp:156
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  if (prev != device) HIP_TRY(hipSetDevice(device));
+  const int64_t n = frames * frame_len;
+  hipLaunchKernelGGL(k_compensate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), reinterpret_cast<const cf*>(in),
+                     reinterpret_cast<cf*>(out), frame_len, frame_stride, frames, Nosr, cfo,
+                     time_offset);
+  hipError_t e = hipGetLastError();
+  if (prev != device) hipSetDevice(prev);
+  if (e != hipSuccess) return set_error(LORA_EIO, std::string("compensate launch: ") + hipGetErrorString(e));
+  return frame_len;
+}
+
+}  // extern "C"

@@ -1,0 +1,141 @@
+// lora_device.h — device building blocks shared by the demod/mod kernels (gfx950).
+//
+// Arithmetic contract: every fp32 operation below is one IEEE operation in the same
+// order as the reference's x86-64 build (no FMA contraction — the file pins
+// `fp contract(off)` and the library is compiled with -ffp-contract=off), so the
+// FFT values, magnitudes and argmax are bit-identical to kissfft<float> /
+// LoRaDetector<float> (include/lora_phy/kissfft.hh, LoRaDetector.hpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lora_libm.h"
+
+#pragma clang fp contract(off)
+
+namespace lora {
+
+struct cf {
+  float re, im;
+};
+
+// Per-frame results of the offset estimate, consumed by every symbol of the frame.
+struct FrameParams {
+  float cfo, toff, rate, scale;
+  int t_off, scaled, pad0, pad1;
+};
+
+// std::complex<float> product as GCC lowers it: (ac - bd, ad + bc).
+__device__ __forceinline__ cf cmul(cf a, cf b) {
+  return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cf cscale(cf a, float s) { return {a.re * s, a.im * s}; }
+
+// kissfft.hh:164-185 kf_bfly4 (forward) on F[0], F[m], F[2m], F[3m].
+__device__ __forceinline__ void bfly4(cf& f0, cf& f1, cf& f2, cf& f3, cf w1, cf w2, cf w3) {
+  const cf s0 = cmul(f1, w1);
+  const cf s1 = cmul(f2, w2);
+  const cf s2 = cmul(f3, w3);
+  const cf s5 = csub(f0, s1);
+  const cf a0 = cadd(f0, s1);
+  const cf s3 = cadd(s0, s2);
+  cf s4 = csub(s0, s2);
+  s4 = cf{s4.im, -s4.re};
+  f2 = csub(a0, s3);
+  f0 = cadd(a0, s3);
+  f1 = cadd(s5, s4);
+  f3 = csub(s5, s4);
+}
+
+// kissfft.hh:155-162 kf_bfly2 (forward).
+__device__ __forceinline__ void bfly2(cf& f0, cf& f1, cf w) {
+  const cf t = cmul(f1, w);
+  const cf a = f0;
+  f1 = csub(a, t);
+  f0 = cadd(a, t);
+}
+
+// Cooperative in-place DIT FFT of G transforms of N = 2^sf points held in LDS in
+// kissfft's leaf order (A[rev[i]] = x[i]).  Stages run bottom-up exactly as
+// kf_work's recursion unwinds: the radix-2 stage (odd sf) first with m = 1, then
+// radix-4 stages with m = 1|2, 4|8, ...  Twiddle for butterfly k of a stage of block
+// size M is tw[q*k*(N/M)] (kissfft.hh:158,169-171).
+__device__ __forceinline__ void fft_lds(cf* A, int sf, int G, const cf* __restrict__ tw, int tid,
+                                        int nthreads) {
+  const int N = 1 << sf;
+  int M = 1;
+  if (sf & 1) {
+    const cf w0 = tw[0];
+    for (int b = tid; b < (G * N) >> 1; b += nthreads) {
+      cf a = A[2 * b], c = A[2 * b + 1];
+      bfly2(a, c, w0);
+      A[2 * b] = a;
+      A[2 * b + 1] = c;
+    }
+    M = 2;
+    __syncthreads();
+  }
+  for (M *= 4; M <= N; M *= 4) {
+    const int m = M >> 2;
+    const int fs = N / M;
+    const int nb = (G * N) >> 2;
+    for (int b = tid; b < nb; b += nthreads) {
+      const int sym = b >> (sf - 2);
+      const int bb = b & ((N >> 2) - 1);
+      const int blk = bb / m;
+      const int k = bb - blk * m;
+      cf* p = A + sym * N + blk * M + k;
+      cf f0 = p[0], f1 = p[m], f2 = p[2 * m], f3 = p[3 * m];
+      bfly4(f0, f1, f2, f3, tw[k * fs], tw[2 * k * fs], tw[3 * k * fs]);
+      p[0] = f0;
+      p[m] = f1;
+      p[2 * m] = f2;
+      p[3 * m] = f3;
+    }
+    __syncthreads();
+  }
+}
+
+// Packed argmax key: |X|^2 bits in the high word (non-negative floats order like
+// their bits; NaN and 0 map to 0, matching the strict '>' scan from maxValue = 0 in
+// LoRaDetector.hpp:46-58), bit-inverted index in the low word so that max() picks
+// the LOWEST index among equal magnitudes (first max wins).
+__device__ __forceinline__ uint64_t argmax_key(cf v, uint32_t idx) {
+  const float m2 = v.re * v.re + v.im * v.im;
+  const float val = (m2 > 0.0f) ? m2 : 0.0f;
+  return ((uint64_t)__float_as_uint(val) << 32) | (uint32_t)(~idx);
+}
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t key_index(uint64_t k) { return ~(uint32_t)k; }
+__device__ __forceinline__ float key_value(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t lo2 = __shfl_xor(lo, mask, 64), hi2 = __shfl_xor(hi, mask, 64);
+  return ((uint64_t)hi2 << 32) | lo2;
+}
+
+// Reduce a key over aligned groups of T lanes (T a power of two <= 64).
+__device__ __forceinline__ uint64_t group_max(uint64_t k, int T) {
+  for (int s = T >> 1; s > 0; s >>= 1) k = umax64(k, shfl_xor64(k, s));
+  return k;
+}
+
+// LoRaDetector.hpp:60-71 for the winning bin: power p and fractional index.
+// `fund2` = max |X|^2, `L`/`R` = the neighbour bins (wrap-around).
+__device__ __forceinline__ void detect_tail(float fund2, cf L, cf R, float power_scale,
+                                            float* p_out, float* findex_out) {
+  const float fundamental = sqrtf(fund2);
+  *p_out = 20.0f * lm_log10f(fundamental) - power_scale;
+  const float left = lm_hypotf(L.re, L.im);
+  const float right = lm_hypotf(R.re, R.im);
+  const double demon = (2.0 * (double)fundamental) - (double)right - (double)left;
+  if (demon == 0.0)
+    *findex_out = 0.0f;
+  else
+    *findex_out = (float)(0.5 * (double)(right - left) / demon);
+}
+
+}  // namespace lora

@@ -1,0 +1,176 @@
+"""GPU demodulation: plan wrapper over lora_demod_batch and the LoRaDemod block.
+
+The plan mirrors ``lora_demod_workspace`` (include/lora_phy/phy.hpp:170-185): it is
+created once per (sf, osr, bw, window, dechirp, mode, device) and holds only constant
+tables on the device.  IQ buffers are torch.complex64 CUDA tensors owned by the
+caller; outputs are allocated with torch's caching allocator (no hipMalloc per call).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _capi
+
+_WINDOWS = {"none": _capi.LORA_WINDOW_NONE, "hann": _capi.LORA_WINDOW_HANN,
+            None: _capi.LORA_WINDOW_NONE, 0: _capi.LORA_WINDOW_NONE, 1: _capi.LORA_WINDOW_HANN}
+_MODES = {"legacy": _capi.LORA_MODE_LEGACY, "api": _capi.LORA_MODE_API}
+
+
+@dataclass
+class DemodResult:
+    """Per-frame results of one batched call (all tensors on the plan's device)."""
+
+    symbols: torch.Tensor      # [F, S] uint16   (LoRaDemod.cpp:165-174)
+    sync: torch.Tensor         # [F] uint8       (LoRaDemod.cpp:177-192)
+    cfo: torch.Tensor          # [F] float32     (lora_metrics.cfo)
+    time_offset: torch.Tensor  # [F] float32     (lora_metrics.time_offset)
+    max_amp: torch.Tensor      # [F] float32     (LoRaDemod.cpp:59-67; 0 in API mode)
+
+
+def _stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_cuda(t: torch.Tensor, name: str) -> None:
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) torch tensor; the product path has no "
+                        "CPU fallback")
+
+
+class DemodPlan:
+    """A device plan for one demodulator configuration (lora_demod_init equivalent)."""
+
+    def __init__(self, sf: int, osr: int = 1, bw: int = 125000, window="none",
+                 dechirp: bool = False, mode: str = "legacy", device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("lora_phy_amd needs a HIP GPU (torch.cuda.is_available() is False)")
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else
+                           torch.device(device).index or 0)
+        self.device = dev
+        self.sf, self.osr, self.bw = int(sf), int(osr) if osr else 1, int(bw)
+        self.N = 1 << self.sf
+        self.step = self.N * self.osr
+        self.window = window
+        self.dechirp = bool(dechirp)
+        self.mode = mode
+        self._lib = _capi.lib()
+        prm = _capi.DemodParams(self.sf, self.osr, self.bw, _WINDOWS[window], int(self.dechirp),
+                                _MODES[mode], dev.index)
+        h = C.c_void_p()
+        _capi.check(self._lib.lora_demod_plan_create(C.byref(prm), C.byref(h)))
+        self._h = h
+        self._ws: Optional[torch.Tensor] = None
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.lora_demod_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def symbols_per_frame(self, frame_len: int) -> int:
+        return _capi.check(self._lib.lora_demod_symbols_per_frame(self._h, int(frame_len)))
+
+    def _workspace(self, frames: int) -> torch.Tensor:
+        need = self._lib.lora_demod_workspace_bytes(self._h, int(frames))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def run(self, iq: torch.Tensor, out: Optional[DemodResult] = None) -> DemodResult:
+        """Demodulate a [F, L] (or [L]) complex64 CUDA tensor; one frame per row."""
+        _require_cuda(iq, "iq")
+        if iq.dtype != torch.complex64:
+            raise TypeError("iq must be complex64 (interleaved fp32 I/Q)")
+        if iq.dim() == 1:
+            iq = iq.unsqueeze(0)
+        if iq.dim() != 2 or iq.stride(1) != 1:
+            raise ValueError("iq must be [frames, samples] with unit sample stride")
+        F, L = iq.shape
+        S = self.symbols_per_frame(L)
+        dev = self.device
+        if out is None:
+            out = DemodResult(
+                symbols=torch.empty((F, max(S, 0)), dtype=torch.uint16, device=dev),
+                sync=torch.empty(F, dtype=torch.uint8, device=dev),
+                cfo=torch.empty(F, dtype=torch.float32, device=dev),
+                time_offset=torch.empty(F, dtype=torch.float32, device=dev),
+                max_amp=torch.zeros(F, dtype=torch.float32, device=dev))
+        ws = self._workspace(F)
+        o = _capi.DemodOutputs(out.symbols.data_ptr() if S > 0 else None,
+                               out.symbols.stride(0) if S > 0 else 0,
+                               out.sync.data_ptr(), out.cfo.data_ptr(), out.time_offset.data_ptr(),
+                               out.max_amp.data_ptr())
+        stride = iq.stride(0) if F > 1 else L
+        _capi.check(self._lib.lora_demod_batch(self._h, iq.data_ptr(), F, L, stride, C.byref(o),
+                                               ws.data_ptr(), ws.numel(), _stream_handle(dev)))
+        return out
+
+    def estimate_offsets(self, iq: torch.Tensor, cfo: torch.Tensor, time_offset: torch.Tensor) -> int:
+        """phy.cpp:78-145 over every whole symbol of each frame (raw samples)."""
+        _require_cuda(iq, "iq")
+        if iq.dim() == 1:
+            iq = iq.unsqueeze(0)
+        F, L = iq.shape
+        stride = iq.stride(0) if F > 1 else L
+        return _capi.check(self._lib.lora_estimate_offsets_batch(
+            self._h, iq.data_ptr(), F, L, stride, cfo.data_ptr(), time_offset.data_ptr(),
+            _stream_handle(self.device)))
+
+
+def compensate_offsets(iq: torch.Tensor, sf: int, osr: int, cfo: torch.Tensor,
+                       time_offset: torch.Tensor) -> torch.Tensor:
+    """phy.cpp:147-176 for a [F, L] batch; returns a new tensor (out of place)."""
+    _require_cuda(iq, "iq")
+    squeeze = iq.dim() == 1
+    x = iq.unsqueeze(0) if squeeze else iq
+    x = x.contiguous()
+    F, L = x.shape
+    out = torch.empty_like(x)
+    lib = _capi.lib()
+    _capi.check(lib.lora_compensate_offsets_batch(
+        int(sf), int(osr), x.data_ptr(), F, L, L, cfo.contiguous().data_ptr(),
+        time_offset.contiguous().data_ptr(), x.device.index, _stream_handle(x.device),
+        out.data_ptr()))
+    return out[0] if squeeze else out
+
+
+class LoRaDemod:
+    """Block-style demodulator mirroring the Pothos ``/lora/lora_demod`` surface
+    (examples/lora_simulation.pth:427-445: sf, sync, thresh, mtu) plus the library
+    parameters bw / cr / osr / window (phy.hpp:51-58).
+
+    ``work(iq)`` consumes one frame (or a [F, L] batch) of raw IQ and returns the
+    symbol stream; per-frame metrics of the last call are in ``last``.
+    """
+
+    def __init__(self, sf: int, sync: int = 0x12, thresh: float = -30.0, mtu: int = 256,
+                 bw: int = 125000, cr: int = 1, osr: int = 1, window="none",
+                 dechirp: bool = True, mode: str = "legacy", device=None):
+        self.sf, self.sync, self.thresh, self.mtu = int(sf), int(sync) & 0xFF, float(thresh), int(mtu)
+        self.bw, self.cr, self.osr = int(bw), int(cr), int(osr) if osr else 1
+        self.plan = DemodPlan(sf, self.osr, bw, window, dechirp, mode, device)
+        self.last: Optional[DemodResult] = None
+
+    def work(self, iq: torch.Tensor) -> torch.Tensor:
+        res = self.plan.run(iq)
+        self.last = res
+        return res.symbols[0] if iq.dim() == 1 else res.symbols
+
+    def work_frames(self, iq: torch.Tensor) -> DemodResult:
+        self.last = self.plan.run(iq)
+        return self.last
+
+    def sync_ok(self) -> torch.Tensor:
+        """Per-frame flag: recovered sync word equals the configured one."""
+        if self.last is None:
+            raise RuntimeError("work() has not run")
+        return self.last.sync == self.sync
