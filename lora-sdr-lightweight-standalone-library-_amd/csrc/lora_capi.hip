@@ -23,16 +23,19 @@
 #include <cmath>
 #include <complex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "../../include/lora_mi355x.h"
 #include "lora_device.h"
+#include "lora_internal.h"
 
 #pragma clang fp contract(off)
 
 using lora::cf;
+using lora::KArgs;
 
 namespace {
 
@@ -150,26 +153,6 @@ __global__ void __launch_bounds__(256) k_frame_max(const cf* __restrict__ iq, in
   }
 }
 
-struct KArgs {
-  const cf* iq;
-  int64_t frame_len, frame_stride;
-  int sf, N, osr, step, total, have_sync, mode, dechirp, hann;
-  float power_scale;
-  const cf* tw;
-  const uint16_t* rev;
-  const float* win;
-  const cf* down;   // legacy dechirp table, `step` entries
-  const cf* down1;  // API per-symbol down-chirp, N entries
-  const uint32_t* maxbits;
-  lora::FrameParams* fp;
-  uint16_t* syms;
-  int64_t sym_stride;
-  uint8_t* sync;
-  float* cfo;
-  float* toff;
-  float* max_amp;
-  int est_only;  // lora_estimate_offsets_batch: all symbols, raw samples, outputs only
-};
 
 // Point i of symbol s of frame f, rotated/windowed, as fed to the detector
 // (LoRaDemod.cpp:142-162; phy.cpp:205-225 for API mode).
@@ -499,6 +482,8 @@ struct lora_demod_plan {
   cf* down1;
   float* win;
   uint16_t* rev;
+  int use_fast;  // 0: generic LDS kernel only (LORA_MI355X_GENERIC=1, for A/B checks)
+  int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), results invalid
   // measurement hooks (lora_demod_profile_enable)
   std::vector<hipEvent_t> prof_ev;  // 4 per recorded call
   int prof_max = 0, prof_calls = 0;
@@ -572,6 +557,12 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   plan->N = N;
   plan->step = step;
   plan->power_scale = 20 * std::log10(static_cast<size_t>(N));  // LoRaDetector.hpp:29
+  {
+    const char* g = std::getenv("LORA_MI355X_GENERIC");
+    plan->use_fast = (g && g[0] == '1') ? 0 : 1;
+    const char* ab = std::getenv("LORA_MI355X_ABLATE");
+    plan->ablate = ab ? std::atoi(ab) : 0;
+  }
   plan->dev_tables = mem;
   plan->tw = reinterpret_cast<cf*>(b);
   b += al(b_tw);
@@ -711,6 +702,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.toff = out->time_offset;
   a.max_amp = out->max_amp;
   a.est_only = 0;
+  a.ablate = plan->ablate;
 
   int rc = LORA_OK;
   prof_record(plan, 0, st);
@@ -739,10 +731,12 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     const int64_t per = total - s0;
     const int64_t work = frames * per;
     if (work > 0) {
-      const int G = std::max(1, 1024 / plan->N);
-      const int64_t grid = (work + G - 1) / G;
-      hipLaunchKernelGGL(k_demod, dim3((unsigned)grid), dim3(256), sizeof(cf) * G * plan->N, st, a,
-                         G, s0, work);
+      if (!plan->use_fast || !lora::launch_demod_fast(a, s0, work, st)) {
+        const int G = std::max(1, 1024 / plan->N);
+        const int64_t grid = (work + G - 1) / G;
+        hipLaunchKernelGGL(k_demod, dim3((unsigned)grid), dim3(256), sizeof(cf) * G * plan->N, st,
+                           a, G, s0, work);
+      }
     }
     prof_record(plan, 3, st);
     if (plan->prof_calls < plan->prof_max) ++plan->prof_calls;

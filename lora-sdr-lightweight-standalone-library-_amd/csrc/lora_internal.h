@@ -1,0 +1,33 @@
+// lora_internal.h — kernel argument block shared by the demod translation units.
+#pragma once
+#include "lora_device.h"
+
+namespace lora {
+
+struct KArgs {
+  const cf* iq;
+  int64_t frame_len, frame_stride;
+  int sf, N, osr, step, total, have_sync, mode, dechirp, hann;
+  float power_scale;
+  const cf* tw;
+  const uint16_t* rev;
+  const float* win;
+  const cf* down;   // legacy dechirp table, `step` entries
+  const cf* down1;  // API per-symbol down-chirp, N entries
+  const uint32_t* maxbits;
+  lora::FrameParams* fp;
+  uint16_t* syms;
+  int64_t sym_stride;
+  uint8_t* sync;
+  float* cfo;
+  float* toff;
+  float* max_amp;
+  int est_only;  // lora_estimate_offsets_batch: all symbols, raw samples, outputs only
+  int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), 0 in production
+};
+
+// Fast symbol demodulator (lora_demod_fast.hip): register-blocked kissfft-exact FFT.
+// Returns false if the configuration is not covered (caller uses the generic kernel).
+bool launch_demod_fast(const KArgs& a, int s0, int64_t work, hipStream_t st);
+
+}  // namespace lora

@@ -168,6 +168,78 @@ LM_FN void lm_sincosf(float y, float* sinp, float* cosp) {
   }
 }
 
+// Branch-free form of lm_sincosf for |y| < 120 (abstop12 < 0x42f).  glibc's |y| < pi/4
+// path equals its reduce_fast path with n = 0 (fma(-0, hpi, x) == x), and its
+// |y| < 2^-12 shortcut (y, 1.0f) equals the polynomial's rounding there except for
+// the sign of -0; so one straight-line sequence reproduces all three.  Checked exhaustively against glibc
+// (tests/test_libm_host.py).
+LM_FN void lm_sincosf_fast(float y, float* sinp, float* cosp) {
+  const double x = (double)y;
+  const double r = x * LM_SC_HPI_INV;
+  const int n = (((int32_t)r) + 0x800000) >> 24;
+  const double xr = lm_fma(-(double)n, LM_SC_HPI, x);
+  const double xs = ((n ^ (n >> 1)) & 1) ? -xr : xr;
+  float s, c;
+  lm_sincosf_poly(xs, xr * xr, (n & 2) != 0, &s, &c);
+  const float sv = (n & 1) ? c : s;
+  *sinp = (y == 0.0f) ? y : sv;  // keep the sign of -0 (glibc's tiny path returns y)
+  *cosp = (n & 1) ? s : c;
+}
+
+// K-way lockstep version of lm_sincosf_fast (identical arithmetic per element).  The
+// element chains are written interleaved so the compiler keeps K independent DP
+// dependency chains in flight instead of one long serial chain per point.
+template <int K>
+LM_FN void lm_sincosf_fast_k(const float* y, float* sinp, float* cosp) {
+  double x[K], xr[K], xs[K], x2[K], x3[K], x4[K], x5[K], x6[K];
+  int n[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) x[k] = (double)y[k];
+#pragma unroll
+  for (int k = 0; k < K; ++k) n[k] = (((int32_t)(x[k] * LM_SC_HPI_INV)) + 0x800000) >> 24;
+#pragma unroll
+  for (int k = 0; k < K; ++k) xr[k] = lm_fma(-(double)n[k], LM_SC_HPI, x[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    xs[k] = ((n[k] ^ (n[k] >> 1)) & 1) ? -xr[k] : xr[k];
+    x2[k] = xr[k] * xr[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    x3[k] = x2[k] * xs[k];
+    x4[k] = x2[k] * x2[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    x5[k] = x2[k] * x3[k];
+    x6[k] = x2[k] * x4[k];
+  }
+  double s1[K], c2[K], c1[K], sp[K], cp[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    s1[k] = lm_fma(x2[k], LM_SC_S3, LM_SC_S2);
+    c2[k] = lm_fma(x2[k], LM_SC_C4, LM_SC_C3);
+    c1[k] = lm_fma(x2[k], LM_SC_C1, LM_SC_C0);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    sp[k] = lm_fma(x3[k], LM_SC_S1, xs[k]);
+    cp[k] = lm_fma(x4[k], LM_SC_C2, c1[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const float sf = (float)lm_fma(s1[k], x5[k], sp[k]);
+    float cf = (float)lm_fma(c2[k], x6[k], cp[k]);
+    if (n[k] & 2) cf = -cf;
+    const float sv = (n[k] & 1) ? cf : sf;
+    sinp[k] = (y[k] == 0.0f) ? y[k] : sv;
+    cosp[k] = (n[k] & 1) ? sf : cf;
+  }
+}
+
+// True when lm_sincosf_fast is exact for y.
+LM_FN int lm_sincosf_fast_ok(float y) { return lm_abstop12(y) < 0x42fu; }
+
 // ---------------------------------------------------------------------------
 // hypotf (glibc 2.35): exact double sum of squares, double sqrt, round to float.
 // ---------------------------------------------------------------------------

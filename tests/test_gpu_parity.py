@@ -84,14 +84,27 @@ CASES = [  # (sf, osr, hann, dechirp, F, symbols-per-frame, extra samples, kind)
 ]
 
 
+def make_plan(amd, path, *args, **kw):
+    """path "fast": register-blocked kernel; "generic": LDS reference kernel (A/B)."""
+    import os
+
+    if path == "generic":
+        os.environ["LORA_MI355X_GENERIC"] = "1"
+    try:
+        return amd.DemodPlan(*args, **kw)
+    finally:
+        os.environ.pop("LORA_MI355X_GENERIC", None)
+
+
+@pytest.mark.parametrize("path", ["fast", "generic"])
 @pytest.mark.parametrize("case", CASES, ids=[f"sf{c[0]}-osr{c[1]}-h{int(c[2])}-d{int(c[3])}-{c[7]}-S{c[5]}"
                                              for c in CASES])
-def test_legacy_demod_matches_oracle(O, amd, case):
+def test_legacy_demod_matches_oracle(O, amd, case, path):
     sf, osr, hann, dechirp, F, nsym, extra, kind = case
     rng = np.random.default_rng(sf * 1000 + osr * 10 + nsym)
     L = nsym * (1 << sf) * osr + extra
     iq = make_frames(O, rng, sf, osr, F, L, kind, dechirp)
-    plan = amd.DemodPlan(sf, osr, 125000, "hann" if hann else "none", dechirp=dechirp)
+    plan = make_plan(amd, path, sf, osr, 125000, "hann" if hann else "none", dechirp=dechirp)
     res = plan.run(torch.from_numpy(iq).cuda())
     torch.cuda.synchronize()
     syms = res.symbols.cpu().numpy()
