@@ -4,7 +4,8 @@
 // Demodulation of F frames is three launches on one stream (generic path, any SF
 // 2..12, any osr, any frame length):
 //   k_frame_max  LEGACY only: per-frame max(|I|,|Q|) of the (dechirped) samples,
-//                LoRaDemod.cpp:59-67, reduced with one atomicMax per workgroup.
+//                LoRaDemod.cpp:59-67, streamed with 16-byte loads, one atomicMax per
+//                workgroup.
 //   k_estimate   one workgroup per frame: the 2-symbol x osr-phase offset estimate
 //                (LoRaDemod.cpp:79-135 / phy.cpp:78-145) and the two sync symbols,
 //                leaving cfo / t_off / rate / scale in the workspace.
@@ -113,6 +114,13 @@ float bw_scale_of(unsigned bw_hz) { return static_cast<float>(bw_hz) / 125000.0f
 
 bool bw_ok(unsigned bw) { return bw == 125000 || bw == 250000 || bw == 500000; }
 
+// Workspace: per-frame max bits and arrival counters (zeroed per batch, 16-byte
+// multiple), then per-frame FrameParams.
+int64_t ws_slots(int64_t frames) { return (frames + 3) & ~int64_t(3); }
+size_t ws_counter_bytes(int64_t frames) {
+  return ((size_t)ws_slots(frames) * 2 * sizeof(uint32_t) + 255) & ~size_t(255);
+}
+
 // ---------------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------------
@@ -126,31 +134,6 @@ __device__ __forceinline__ cf load_legacy(const cf* __restrict__ x, int64_t j,
   if (dechirp) v = lora::cmul(v, down[j % step]);
   if (scaled) v = lora::cscale(v, scale);
   return v;
-}
-
-__global__ void __launch_bounds__(256) k_frame_max(const cf* __restrict__ iq, int64_t frame_len,
-                                                   int64_t frame_stride, int bpf, int chunk,
-                                                   const cf* __restrict__ down, int step,
-                                                   int dechirp, uint32_t* __restrict__ maxbits) {
-  const int64_t f = blockIdx.x / bpf;
-  const int64_t c = blockIdx.x % bpf;
-  const cf* x = iq + f * frame_stride;
-  const int64_t j0 = c * (int64_t)chunk;
-  const int64_t j1 = min(j0 + (int64_t)chunk, frame_len);
-  float m = 0.0f;
-  for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
-    const cf v = load_legacy(x, j, down, step, dechirp, 0, 1.0f);
-    m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
-  }
-  for (int s = 32; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s, 64));
-  __shared__ float wmax[4];
-  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float r = wmax[0];
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) r = fmaxf(r, wmax[w]);
-    if (r > 0.0f) atomicMax(&maxbits[f], __float_as_uint(r));
-  }
 }
 
 
@@ -195,27 +178,16 @@ __device__ __forceinline__ uint64_t wg_argmax(const cf* A, int N, uint64_t* red)
   return r;
 }
 
-__global__ void __launch_bounds__(256) k_estimate(KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  cf* A = reinterpret_cast<cf*>(smem);
+// Offset estimate (LoRaDemod.cpp:79-135 / phy.cpp:78-145) and the two sync symbols
+// of frame f, by the whole workgroup (A: N-complex LDS FFT buffer).  `scaled`/`scale`
+// carry the normalisation decision (LoRaDemod.cpp:68-77), `maxv` the frame max.
+__device__ __forceinline__ void estimate_frame(const KArgs& a, int f, int scaled, float scale,
+                                            float maxv, cf* A) {
   __shared__ uint64_t red[4];
   __shared__ lora::FrameParams sp;
   __shared__ uint16_t sw[2];
-  const int f = blockIdx.x;
   const cf* x = a.iq + (int64_t)f * a.frame_stride;
   const int N = a.N;
-
-  // Normalisation decision (LoRaDemod.cpp:68-77); API mode never normalises.
-  float scale = 1.0f;
-  int scaled = 0;
-  float maxv = 0.0f;
-  if (a.mode == LORA_MODE_LEGACY && !a.est_only) {
-    maxv = __uint_as_float(a.maxbits[f]);
-    if (maxv > 1.0f) {
-      scaled = 1;
-      scale = 1.0f / maxv;
-    }
-  }
   const bool raw = a.mode == LORA_MODE_API || a.est_only;
   const int est = a.est_only ? a.total : (a.mode == LORA_MODE_API) ? 2 : min(a.total, 2);
   const bool tie_rule = a.mode == LORA_MODE_LEGACY && !a.est_only;
@@ -324,6 +296,90 @@ __global__ void __launch_bounds__(256) k_estimate(KArgs a) {
     }
   } else if (threadIdx.x == 0 && a.sync) {
     a.sync[f] = 0;
+  }
+}
+
+// One workgroup per frame.  LEGACY: the normalisation decision from k_frame_max's
+// per-frame maximum; API mode / lora_estimate_offsets_batch: raw samples.
+__global__ void __launch_bounds__(256) k_estimate(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float maxv = 0.0f;
+  if (a.mode == LORA_MODE_LEGACY && !a.est_only) maxv = __uint_as_float(a.maxbits[blockIdx.x]);
+  const int scaled = maxv > 1.0f;
+  estimate_frame(a, blockIdx.x, scaled, scaled ? 1.0f / maxv : 1.0f, maxv,
+                 reinterpret_cast<cf*>(smem));
+}
+
+// LEGACY: per-frame max(|I|,|Q|) of the (dechirped) samples (LoRaDemod.cpp:59-67),
+// streamed by `bpf` blocks per frame (`chunk` samples each, 16-byte loads) and reduced
+// with one atomicMax per block into maxbits (zeroed before the launch).
+__global__ void __launch_bounds__(256) k_frame_max(KArgs a, int bpf, int chunk,
+                                                   uint32_t* __restrict__ maxbits) {
+  __shared__ float wmax[4];
+  const int64_t f = blockIdx.x / bpf;
+  const int64_t c = blockIdx.x - f * bpf;
+  const int64_t fb = f * a.frame_stride;
+  const cf* x = a.iq + fb;
+  const int step = a.step;
+  const int64_t j0 = c * (int64_t)chunk;
+  const int64_t j1 = min(j0 + (int64_t)chunk, a.frame_len);
+  float m = 0.0f;
+  if ((fb & 1) == 0) {  // 16-byte aligned frame (chunk starts are even)
+    // Batches of KB pairs per thread: all IQ loads, then all table loads, then the
+    // math, so each batch costs one memory round trip.
+    constexpr int KB = 8;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const int64_t p0 = j0 >> 1, p1 = j1 >> 1;
+    const int stride = (int)blockDim.x;
+    int d = (int)((j0 + 2 * (int64_t)threadIdx.x) % step);
+    const int inc = (2 * stride) % step;
+    for (int64_t pb = p0 + threadIdx.x; pb < p1; pb += (int64_t)KB * stride) {
+      f4v q[KB];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const int64_t pr = pb + (int64_t)k * stride;
+        q[k] = pr < p1 ? *reinterpret_cast<const f4v*>(x + 2 * pr) : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+      if (a.dechirp) {
+        cf w0[KB], w1[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const int d1 = (d + 1 == step) ? 0 : d + 1;
+          w0[k] = a.down[d];
+          w1[k] = a.down[d1];
+          d += inc;
+          if (d >= step) d -= step;
+        }
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const cf v0 = lora::cmul(cf{q[k][0], q[k][1]}, w0[k]);
+          const cf v1 = lora::cmul(cf{q[k][2], q[k][3]}, w1[k]);
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(v0.re), fabsf(v0.im)), fmaxf(fabsf(v1.re), fabsf(v1.im))));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < KB; ++k)
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(q[k][0]), fabsf(q[k][1])), fmaxf(fabsf(q[k][2]), fabsf(q[k][3]))));
+      }
+    }
+    if ((j1 & 1) && threadIdx.x == 0) {  // odd end of the frame
+      cf v = x[j1 - 1];
+      if (a.dechirp) v = lora::cmul(v, a.down[(j1 - 1) % step]);
+      m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+    }
+  } else {
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+      cf v = x[j];
+      if (a.dechirp) v = lora::cmul(v, a.down[j % step]);
+      m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float r = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    if (r > 0.0f) atomicMax(&maxbits[f], __float_as_uint(r));
   }
 }
 
@@ -644,8 +700,7 @@ int64_t lora_demod_symbols_per_frame(const lora_demod_plan* plan, int64_t frame_
 size_t lora_demod_workspace_bytes(const lora_demod_plan* plan, int64_t frames) {
   (void)plan;
   if (frames <= 0) return 0;
-  const size_t mb = ((size_t)frames * sizeof(uint32_t) + 255) & ~size_t(255);
-  return mb + (size_t)frames * sizeof(lora::FrameParams);
+  return ws_counter_bytes(frames) + (size_t)frames * sizeof(lora::FrameParams);
 }
 
 int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames, int64_t frame_len,
@@ -694,7 +749,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   unsigned char* wsb = static_cast<unsigned char*>(workspace);
   uint32_t* maxbits = reinterpret_cast<uint32_t*>(wsb);
   a.maxbits = maxbits;
-  a.fp = reinterpret_cast<lora::FrameParams*>(wsb + (((size_t)frames * 4 + 255) & ~size_t(255)));
+  a.fp = reinterpret_cast<lora::FrameParams*>(wsb + ws_counter_bytes(frames));
   a.syms = out->symbols;
   a.sym_stride = out->sym_stride;
   a.sync = out->sync;
@@ -708,21 +763,20 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   prof_record(plan, 0, st);
   do {
     if (p.mode == LORA_MODE_LEGACY) {
-      if (hipMemsetAsync(maxbits, 0, (size_t)frames * 4, st) != hipSuccess) {
+      // Frame max streamed by several blocks per frame, then the estimate.
+      if (hipMemsetAsync(maxbits, 0, ws_counter_bytes(frames), st) != hipSuccess) {
         rc = set_error(LORA_EIO, "hipMemsetAsync failed");
         break;
       }
-      if (frame_len > 0) {
-        const int chunk = 4096;
-        const int bpf = (int)((frame_len + chunk - 1) / chunk);
-        const int64_t grid = frames * bpf;
-        if (grid >= (int64_t(1) << 31)) {
-          rc = set_error(LORA_EINVAL, "batch too large");
-          break;
-        }
-        hipLaunchKernelGGL(k_frame_max, dim3((unsigned)grid), dim3(256), 0, st, a.iq, frame_len,
-                           frame_stride, bpf, chunk, a.down, a.step, a.dechirp, maxbits);
+      // <= 8 pairs per thread per block (one batch of k_frame_max), split evenly
+      const int bpf = frame_len > 0 ? (int)((frame_len + 4095) / 4096) : 1;
+      const int chunk = (int)((((frame_len + bpf - 1) / bpf) + 1) & ~int64_t(1));
+      const int64_t grid = frames * bpf;
+      if (grid >= (int64_t(1) << 31)) {
+        rc = set_error(LORA_EINVAL, "batch too large");
+        break;
       }
+      hipLaunchKernelGGL(k_frame_max, dim3((unsigned)grid), dim3(256), 0, st, a, bpf, chunk, maxbits);
     }
     prof_record(plan, 1, st);
     hipLaunchKernelGGL(k_estimate, dim3((unsigned)frames), dim3(256), sizeof(cf) * plan->N, st, a);
