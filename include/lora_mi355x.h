@@ -25,8 +25,10 @@
  * (I,Q) pairs — the layout of std::complex<float> and torch.complex64 — and live in
  * device memory (HBM) of the plan's device.  The caller owns every buffer
  * (API_SPEC.md ownership rule); the plan owns only its constant tables.  No call
- * allocates or synchronises: `stream` is a hipStream_t (NULL = default stream) and
- * all work is enqueued on it, so the calls are hipGraph-capturable.
+ * allocates or synchronises: `stream` is a hipStream_t (NULL = default stream); the
+ * work is enqueued on it (lora_demod_batch forks large batches onto the plan's
+ * auxiliary stream and joins back with events), so the calls are hipGraph-capturable.
+ * A plan may be used by one host thread at a time.
  *
  * Errors are negative errno values (the reference returns -1, phy.cpp:27,58,181-190);
  * lora_last_error() gives a thread-local message.
@@ -131,12 +133,15 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
                        const uint16_t* symbols, int64_t frames, int64_t sym_count, float* iq,
                        int device, void* stream);
 
-/* Measurement hooks (bench.py): while enabled, every lora_demod_batch call on this
- * plan records a HIP event before its first launch and after each of its stages
- * (0 = frame max, 1 = estimate + sync symbols, 2 = symbol demod) on its stream, for
- * up to `max_calls` calls.  lora_demod_profile_read waits for the last recorded
- * event and returns, per stage, the summed elapsed ms over the recorded calls
- * (stage_ms[3]) and the number of calls recorded.  No effect on results. */
+/* Measurement hooks (bench.py): while enabled, every kernel lora_demod_batch launches
+ * on this plan is bracketed by a pair of HIP events on the stream it runs on, for up
+ * to `max_calls` calls.  Stages: 0 = frame max, 1 = estimate + sync symbols,
+ * 2 = symbol demod.  lora_demod_profile_read waits for the recorded events and
+ * returns, per stage, the summed kernel ms over the recorded calls (stage_ms[3]) and
+ * the number of calls recorded.  Large batches are pipelined in chunks (prep of
+ * chunk c+1 on the plan's auxiliary stream overlaps demod of chunk c on `stream`),
+ * so stage times can overlap and need not add up to the wall time.  No effect on
+ * results. */
 int lora_demod_profile_enable(lora_demod_plan* plan, int max_calls);
 int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls);
 

@@ -540,16 +540,47 @@ struct lora_demod_plan {
   uint16_t* rev;
   int use_fast;  // 0: generic LDS kernel only (LORA_MI355X_GENERIC=1, for A/B checks)
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), results invalid
-  // measurement hooks (lora_demod_profile_enable)
-  std::vector<hipEvent_t> prof_ev;  // 4 per recorded call
+  int max_chunks;  // 2-stream pipeline depth (LORA_MI355X_CHUNKS, default 1 = off)
+  // Two-stream pipeline: per-frame prep (max + estimate) of chunk c+1 on `aux`
+  // overlaps the symbol demod of chunk c on the caller's stream.
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_chunk[16] = {};
+  // measurement hooks (lora_demod_profile_enable): per kernel launch (stage, begin, end)
+  struct ProfRec {
+    int stage;
+    hipEvent_t b, e;
+  };
+  std::vector<hipEvent_t> prof_pool;
+  std::vector<ProfRec> prof_recs;
   int prof_max = 0, prof_calls = 0;
 };
 
 namespace {
-void prof_record(lora_demod_plan* plan, int stage, hipStream_t st) {
-  if (plan->prof_calls >= plan->prof_max) return;
-  hipEventRecord(plan->prof_ev[(size_t)plan->prof_calls * 4 + stage], st);
-}
+constexpr int kMaxChunks = 16;
+
+// Event pair around one kernel launch (profiling only; no-op when disabled).
+struct ProfScope {
+  lora_demod_plan* plan;
+  hipStream_t st;
+  int stage;
+  bool on;
+  hipEvent_t e = nullptr;
+  ProfScope(lora_demod_plan* p, int s, hipStream_t stream) : plan(p), st(stream), stage(s) {
+    on = plan->prof_calls < plan->prof_max && plan->prof_pool.size() >= 2;
+    if (on) {
+      hipEvent_t b = plan->prof_pool.back();
+      plan->prof_pool.pop_back();
+      e = plan->prof_pool.back();
+      plan->prof_pool.pop_back();
+      hipEventRecord(b, st);
+      plan->prof_recs.push_back({stage, b, e});
+    }
+  }
+  ~ProfScope() {
+    if (on) hipEventRecord(e, st);
+  }
+};
 }  // namespace
 
 extern "C" {
@@ -618,6 +649,8 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
     plan->use_fast = (g && g[0] == '1') ? 0 : 1;
     const char* ab = std::getenv("LORA_MI355X_ABLATE");
     plan->ablate = ab ? std::atoi(ab) : 0;
+    const char* ch = std::getenv("LORA_MI355X_CHUNKS");
+    plan->max_chunks = std::max(1, std::min(kMaxChunks, ch ? std::atoi(ch) : 1));
   }
   plan->dev_tables = mem;
   plan->tw = reinterpret_cast<cf*>(b);
@@ -629,7 +662,11 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   plan->win = reinterpret_cast<float*>(b);
   b += al(b_win);
   plan->rev = reinterpret_cast<uint16_t*>(b);
-  hipError_t e = hipMemcpy(plan->tw, tw.data(), b_tw, hipMemcpyHostToDevice);
+  hipError_t e = hipStreamCreateWithFlags(&plan->aux, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->ev_fork, hipEventDisableTiming);
+  for (int c = 0; c < kMaxChunks && e == hipSuccess; ++c)
+    e = hipEventCreateWithFlags(&plan->ev_chunk[c], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMemcpy(plan->tw, tw.data(), b_tw, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->down, down.data(), b_down, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->down1, down1.data(), b_down1, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->win, win.data(), b_win, hipMemcpyHostToDevice);
@@ -649,9 +686,14 @@ int lora_demod_profile_enable(lora_demod_plan* plan, int max_calls) {
   int prev = 0;
   HIP_TRY(hipGetDevice(&prev));
   HIP_TRY(hipSetDevice(plan->prm.device));
-  for (hipEvent_t e : plan->prof_ev) hipEventDestroy(e);
-  plan->prof_ev.assign((size_t)max_calls * 4, nullptr);
-  for (auto& e : plan->prof_ev) HIP_TRY(hipEventCreate(&e));
+  for (auto& r : plan->prof_recs) {
+    hipEventDestroy(r.b);
+    hipEventDestroy(r.e);
+  }
+  for (hipEvent_t e : plan->prof_pool) hipEventDestroy(e);
+  plan->prof_recs.clear();
+  plan->prof_pool.assign((size_t)max_calls * 3 * kMaxChunks * 2, nullptr);
+  for (auto& e : plan->prof_pool) HIP_TRY(hipEventCreate(&e));
   plan->prof_max = max_calls;
   plan->prof_calls = 0;
   HIP_TRY(hipSetDevice(prev));
@@ -662,14 +704,12 @@ int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls) 
   if (!plan || !stage_ms || !calls) return set_error(LORA_EINVAL, "bad argument");
   for (int k = 0; k < 3; ++k) stage_ms[k] = 0.0f;
   *calls = plan->prof_calls;
-  if (plan->prof_calls == 0) return LORA_OK;
-  HIP_TRY(hipEventSynchronize(plan->prof_ev[(size_t)plan->prof_calls * 4 - 1]));
-  for (int c = 0; c < plan->prof_calls; ++c)
-    for (int k = 0; k < 3; ++k) {
-      float ms = 0.0f;
-      HIP_TRY(hipEventElapsedTime(&ms, plan->prof_ev[(size_t)c * 4 + k], plan->prof_ev[(size_t)c * 4 + k + 1]));
-      stage_ms[k] += ms;
-    }
+  for (auto& r : plan->prof_recs) {
+    HIP_TRY(hipEventSynchronize(r.e));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, r.b, r.e));
+    if (r.stage >= 0 && r.stage < 3) stage_ms[r.stage] += ms;
+  }
   return LORA_OK;
 }
 
@@ -678,7 +718,15 @@ int lora_demod_plan_destroy(lora_demod_plan* plan) {
   int prev = 0;
   hipGetDevice(&prev);
   hipSetDevice(plan->prm.device);
-  for (hipEvent_t e : plan->prof_ev) hipEventDestroy(e);
+  for (auto& r : plan->prof_recs) {
+    hipEventDestroy(r.b);
+    hipEventDestroy(r.e);
+  }
+  for (hipEvent_t e : plan->prof_pool) hipEventDestroy(e);
+  if (plan->aux) hipStreamDestroy(plan->aux);
+  if (plan->ev_fork) hipEventDestroy(plan->ev_fork);
+  for (hipEvent_t e : plan->ev_chunk)
+    if (e) hipEventDestroy(e);
   hipFree(plan->dev_tables);
   hipSetDevice(prev);
   delete plan;
@@ -759,44 +807,80 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.est_only = 0;
   a.ablate = plan->ablate;
 
+  const int s0 = a.have_sync ? 2 : 0;
+  const int64_t per = total - s0;
+  const int bpf = frame_len > 0 ? (int)((frame_len + 4095) / 4096) : 1;
+  // <= 8 pairs per thread per block (one batch of k_frame_max), split evenly
+  const int chunk = (int)((((frame_len + bpf - 1) / bpf) + 1) & ~int64_t(1));
+  if (frames * bpf >= (int64_t(1) << 31)) {
+    if (prev != p.device) hipSetDevice(prev);
+    return set_error(LORA_EINVAL, "batch too large");
+  }
+  // Per-frame prep of one chunk: (LEGACY) frame max, then estimate + sync symbols.
+  auto prep = [&](const KArgs& ac, uint32_t* mb, int64_t nf, hipStream_t s) {
+    if (p.mode == LORA_MODE_LEGACY && frame_len > 0) {
+      ProfScope ps(plan, 0, s);
+      hipLaunchKernelGGL(k_frame_max, dim3((unsigned)(nf * bpf)), dim3(256), 0, s, ac, bpf, chunk, mb);
+    }
+    ProfScope ps(plan, 1, s);
+    hipLaunchKernelGGL(k_estimate, dim3((unsigned)nf), dim3(256), sizeof(cf) * plan->N, s, ac);
+  };
+  auto demod = [&](const KArgs& ac, int64_t nf, hipStream_t s) {
+    const int64_t work = nf * per;
+    if (work <= 0) return;
+    ProfScope ps(plan, 2, s);
+    if (!plan->use_fast || !lora::launch_demod_fast(ac, s0, work, s)) {
+      const int G = std::max(1, 1024 / plan->N);
+      hipLaunchKernelGGL(k_demod, dim3((unsigned)((work + G - 1) / G)), dim3(256),
+                         sizeof(cf) * G * plan->N, s, ac, G, s0, work);
+    }
+  };
+  auto chunk_args = [&](int64_t c0) {
+    KArgs ac = a;
+    ac.iq = a.iq + c0 * frame_stride;
+    ac.maxbits = a.maxbits + c0;
+    ac.fp = a.fp + c0;
+    if (ac.syms) ac.syms = a.syms + c0 * a.sym_stride;
+    if (ac.sync) ac.sync = a.sync + c0;
+    if (ac.cfo) ac.cfo = a.cfo + c0;
+    if (ac.toff) ac.toff = a.toff + c0;
+    if (ac.max_amp) ac.max_amp = a.max_amp + c0;
+    return ac;
+  };
+  const int nchunks = (int)std::min<int64_t>(plan->max_chunks, frames / 1024);
   int rc = LORA_OK;
-  prof_record(plan, 0, st);
-  do {
-    if (p.mode == LORA_MODE_LEGACY) {
-      // Frame max streamed by several blocks per frame, then the estimate.
-      if (hipMemsetAsync(maxbits, 0, ws_counter_bytes(frames), st) != hipSuccess) {
-        rc = set_error(LORA_EIO, "hipMemsetAsync failed");
-        break;
-      }
-      // <= 8 pairs per thread per block (one batch of k_frame_max), split evenly
-      const int bpf = frame_len > 0 ? (int)((frame_len + 4095) / 4096) : 1;
-      const int chunk = (int)((((frame_len + bpf - 1) / bpf) + 1) & ~int64_t(1));
-      const int64_t grid = frames * bpf;
-      if (grid >= (int64_t(1) << 31)) {
-        rc = set_error(LORA_EINVAL, "batch too large");
-        break;
-      }
-      hipLaunchKernelGGL(k_frame_max, dim3((unsigned)grid), dim3(256), 0, st, a, bpf, chunk, maxbits);
+  if (nchunks <= 1) {
+    if (p.mode == LORA_MODE_LEGACY && hipMemsetAsync(maxbits, 0, ws_counter_bytes(frames), st) != hipSuccess)
+      rc = set_error(LORA_EIO, "hipMemsetAsync failed");
+    if (rc == LORA_OK) {
+      prep(a, maxbits, frames, st);
+      demod(a, frames, st);
     }
-    prof_record(plan, 1, st);
-    hipLaunchKernelGGL(k_estimate, dim3((unsigned)frames), dim3(256), sizeof(cf) * plan->N, st, a);
-    prof_record(plan, 2, st);
-    const int s0 = a.have_sync ? 2 : 0;
-    const int64_t per = total - s0;
-    const int64_t work = frames * per;
-    if (work > 0) {
-      if (!plan->use_fast || !lora::launch_demod_fast(a, s0, work, st)) {
-        const int G = std::max(1, 1024 / plan->N);
-        const int64_t grid = (work + G - 1) / G;
-        hipLaunchKernelGGL(k_demod, dim3((unsigned)grid), dim3(256), sizeof(cf) * G * plan->N, st,
-                           a, G, s0, work);
-      }
+  } else {
+    // fork: aux waits for the caller's prior work, runs every chunk's prep; the
+    // caller's stream joins chunk by chunk before each demod (capturable pattern).
+    hipStream_t ax = plan->aux;
+    hipEventRecord(plan->ev_fork, st);
+    hipStreamWaitEvent(ax, plan->ev_fork, 0);
+    if (p.mode == LORA_MODE_LEGACY && hipMemsetAsync(maxbits, 0, ws_counter_bytes(frames), ax) != hipSuccess)
+      rc = set_error(LORA_EIO, "hipMemsetAsync failed");
+    const int64_t fpc = (frames + nchunks - 1) / nchunks;
+    for (int c = 0; c < nchunks && rc == LORA_OK; ++c) {
+      const int64_t c0 = c * fpc, nf = std::min(fpc, frames - c0);
+      if (nf > 0) prep(chunk_args(c0), maxbits + c0, nf, ax);
+      hipEventRecord(plan->ev_chunk[c], ax);
     }
-    prof_record(plan, 3, st);
-    if (plan->prof_calls < plan->prof_max) ++plan->prof_calls;
+    for (int c = 0; c < nchunks && rc == LORA_OK; ++c) {
+      const int64_t c0 = c * fpc, nf = std::min(fpc, frames - c0);
+      hipStreamWaitEvent(st, plan->ev_chunk[c], 0);
+      if (nf > 0) demod(chunk_args(c0), nf, st);
+    }
+  }
+  if (plan->prof_calls < plan->prof_max) ++plan->prof_calls;
+  if (rc == LORA_OK) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) rc = set_error(LORA_EIO, std::string("kernel launch: ") + hipGetErrorString(e));
-  } while (0);
+  }
   if (prev != p.device) hipSetDevice(prev);
   return rc < 0 ? rc : nsym;
 }
