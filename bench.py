@@ -31,6 +31,7 @@ sys.path.insert(0, REPO)
 
 import lora_phy_amd as amd  # noqa: E402
 from lora_phy_amd import _capi  # noqa: E402
+from lora_phy_amd.shard import aggregate_throughput  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 METRIC = "Msymbols/s dechirp+FFT+argmax @ SF7 & SF12, 1/2/4/8 GPU; % HBM roofline"
@@ -73,8 +74,6 @@ def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=
     for _ in range(warmup):
         out = plan.run(iq, out)
     torch.cuda.synchronize(device)
-    lib = _capi.lib()
-    _capi.check(lib.lora_demod_profile_enable(plan._h, steps))
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -85,17 +84,22 @@ def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=
     if dist is not None:
         dist.barrier()
     wall = time.perf_counter() - t0
+    # Per-kernel durations: a second pass of the same steps with HIP events around every
+    # launch, recorded on the stream each kernel runs on (not inside the timed region).
     import ctypes as C
 
+    lib = _capi.lib()
+    _capi.check(lib.lora_demod_profile_enable(plan._h, steps))
+    for _ in range(steps):
+        out = plan.run(iq, out)
+    torch.cuda.synchronize(device)
     stage = (C.c_float * 3)()
     calls = C.c_int()
     _capi.check(lib.lora_demod_profile_read(plan._h, stage, C.byref(calls)))
     lib.lora_demod_profile_enable(plan._h, 0)
     stage_ms = [stage[k] / max(calls.value, 1) for k in range(3)]
-    t = torch.tensor([wall], dtype=torch.float64, device=device)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
+    # weak scaling: every rank owns its frames; units summed, time = max over ranks
+    units, wall, _ = aggregate_throughput(frames * data_syms * steps, wall)
     ok = bool(torch.equal(out.symbols.to(torch.int32).cpu(), syms)) if snr_db is None else None
     total_syms = data_syms + 2
     ms_step = wall * 1e3 / steps
@@ -109,6 +113,7 @@ def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=
         "sf": sf, "frames": frames, "data_symbols": frames * data_syms, "iq_bytes": iq.numel() * 8,
         "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ok,
         "msym_s_data": frames * data_syms / (ms_step * 1e-3) / 1e6,
+        "msym_s_all_ranks": units / wall / 1e6,
         "msym_s_all": frames * total_syms / (ms_step * 1e-3) / 1e6,
         "dominant_kernel": "k_demod", "dominant_gbs": dom_gbs,
         "dominant_bytes_per_launch": demod_bytes,
@@ -117,24 +122,33 @@ def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=
     }
 
 
-def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=20.0):
-    from oracle.pyoracle import Oracle
+def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=2.0):
+    """The reference's own lora_demodulate (oracle/_ref, compiled from the reference's
+    sources, travels with the snapshot) on `threads` host cores over a bounded sample of
+    the same frames; falls back to the restatement (oracle/lora_oracle.cpp) if absent.
+    Sample: whole passes over the first `max_frames` frames until `time_budget_s` wall
+    seconds have elapsed (~30 CPU-seconds at 16 threads)."""
+    from oracle.pyoracle import Oracle, Reference
 
-    O = Oracle()
+    if Reference.available():
+        impl, kind, what = Reference(), "reference", "reference src/phy lora_demodulate (oracle/_ref)"
+    else:
+        impl, kind, what = Oracle(), "port", "restatement oracle/lora_oracle.cpp"
     F = min(iq_dev.shape[0], max_frames)
     x = iq_dev[:F].cpu().numpy()
+    impl.demod_frames(x[: min(F, 4 * threads)], sf, 1, False, dechirp=True, threads=threads)  # warm
     t0 = time.perf_counter()
     done = 0
     while True:
-        O.demod_frames(x, sf, 1, False, dechirp=True, threads=threads)
+        impl.demod_frames(x, sf, 1, False, dechirp=True, threads=threads)
         done += F
-        if time.perf_counter() - t0 > time_budget_s / 4 or done >= 4 * F:
+        if time.perf_counter() - t0 > time_budget_s:
             break
     dt = time.perf_counter() - t0
     rate = done * data_syms / dt / 1e6
-    return {"value": rate, "unit": "Msymbols/s", "cores": threads, "kind": "port",
-            "sample": f"{done} frames (SF{sf}, {data_syms}+2 symbols each, dechirp+lora_demodulate "
-                      f"restatement oracle/lora_oracle.cpp, {threads} threads, {dt:.2f} s)"}
+    return {"value": rate, "unit": "Msymbols/s", "cores": threads, "kind": kind,
+            "sample": f"{done} frames of the SF{sf} bench batch ({data_syms}+2 symbols each), "
+                      f"caller-side dechirp + {what}, {threads} threads, {dt:.2f} s"}
 
 
 def load_pmc(workload):
@@ -157,19 +171,26 @@ def main():
     ap.add_argument("--data-symbols", type=int, default=64)
     ap.add_argument("--sf12-frames", type=int, default=15625)
     ap.add_argument("--no-sf12", action="store_true")
+    ap.add_argument("--sf12-only", action="store_true", help="profiling: SF12 workload only")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
 
     dist, rank, world = dist_setup(args.gpus)
     device = torch.device("cuda", torch.cuda.current_device())
+    if args.sf12_only:
+        r12 = run_config(12, args.sf12_frames, args.data_symbols, args.steps, args.warmup, rank, dist,
+                         device)
+        if rank == 0:
+            print(json.dumps({k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host")}))
+        return
     r7 = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, rank, dist, device)
     extra = {}
     if not args.no_sf12:
         r12 = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2),
                          args.warmup, rank, dist, device)
         extra["sf12"] = {k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host")}
-        extra["sf12"]["value_all_ranks_msym_s"] = r12["msym_s_data"] * world
+        extra["sf12"]["value_all_ranks_msym_s"] = r12["msym_s_all_ranks"]
         extra["sf12"]["roofline_frac"] = r12["dominant_gbs"] / HBM_PEAK_GBS
         del r12
         torch.cuda.empty_cache()
@@ -184,7 +205,7 @@ def main():
                     f"(2 sync + {args.data_symbols} data) symbols per GPU, noiseless")
         line = {
             "metric": METRIC,
-            "value": r7["msym_s_data"] * world,
+            "value": r7["msym_s_all_ranks"],
             "unit": "Msymbols/s",
             "n_gpus": world,
             "steps": args.steps,

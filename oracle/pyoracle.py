@@ -6,8 +6,8 @@ bench.py's cpu_baseline leg.  The product package (lora_phy_amd) never imports t
 * ``Oracle`` wraps ``oracle/liblora_oracle.so`` - the C++ restatement of the reference
   hot path (oracle/lora_oracle.cpp), available everywhere including the GPU box.
 * ``Reference`` wraps ``oracle/_ref/liblora_ref.so`` - the reference library itself,
-  compiled from /root/reference by oracle/Makefile.  Only exists in the build
-  container; ``Reference.available()`` tells.
+  compiled from /root/reference by oracle/Makefile in the build container (the built
+  .so travels to the GPU box with the repo snapshot); ``Reference.available()`` tells.
 """
 from __future__ import annotations
 
@@ -55,7 +55,8 @@ class _Common:
     def gen_chirp(self, N, osr, NN, f0, down, ampl, phase, bw_scale):
         out = np.empty(NN, np.complex64)
         ph = C.c_float(phase)
-        getattr(self.lib, self.prefix + "gen_chirp")(out.view(np.float32), N, osr, NN, C.c_float(f0),
+        getattr(self.lib, self.prefix + "gen_chirp")(out.ctypes.data_as(C.c_void_p), N, osr, NN,
+                                                     C.c_float(f0),
                                                      int(down), C.c_float(ampl), C.byref(ph),
                                                      C.c_float(bw_scale))
         return out, ph.value
@@ -131,6 +132,22 @@ class _Common:
                                                               C.c_float(cfo), C.c_float(to))
         return x
 
+    def demod_frames(self, iq2d, sf, osr=1, hann=False, dechirp=False, bw=125000, threads=1):
+        """Legacy lora_demodulate over a [F, L] complex64 batch (one call per frame)."""
+        x = _c64(iq2d)
+        F, L = x.shape
+        total = L // ((1 << sf) * osr)
+        stride = max(total, 1)
+        syms = np.zeros((F, stride), np.uint16)
+        sync = np.zeros(F, np.uint8)
+        cfo = np.zeros(F, np.float32)
+        toff = np.zeros(F, np.float32)
+        cnt = np.zeros(F, np.int64)
+        getattr(self.lib, self.prefix + "demod_frames")(
+            x.reshape(-1).view(np.float32), F, L, sf, int(hann), osr, int(dechirp), BW_SCALE[bw],
+            syms, stride, sync, cfo, toff, cnt, threads)
+        return syms, sync, cfo, toff, cnt
+
 
 class Oracle(_Common):
     prefix = "orc_"
@@ -179,22 +196,6 @@ class Oracle(_Common):
                              BW_SCALE[bw])
         return y
 
-    def demod_frames(self, iq2d, sf, osr=1, hann=False, dechirp=False, bw=125000, threads=1):
-        """Legacy lora_demodulate over a [F, L] complex64 batch (one call per frame)."""
-        x = _c64(iq2d)
-        F, L = x.shape
-        total = L // ((1 << sf) * osr)
-        stride = max(total, 1)
-        syms = np.zeros((F, stride), np.uint16)
-        sync = np.zeros(F, np.uint8)
-        cfo = np.zeros(F, np.float32)
-        toff = np.zeros(F, np.float32)
-        cnt = np.zeros(F, np.int64)
-        self.lib.orc_demod_frames(x.reshape(-1).view(np.float32), F, L, sf, int(hann), osr,
-                                  int(dechirp), BW_SCALE[bw], syms, stride, sync, cfo, toff, cnt,
-                                  threads)
-        return syms, sync, cfo, toff, cnt
-
     def awgn_gtest_frames(self, profiles, packets=5, payload_size=16, snr_db=12.0):
         sfs = (C.c_uint * len(profiles))(*[p[0] for p in profiles])
         bws = (C.c_float * len(profiles))(*[BW_SCALE[p[1]] for p in profiles])
@@ -237,6 +238,9 @@ class Reference(_Common):
         L.ref_lora_decode.restype = C.c_size_t
         L.ref_lora_decode.argtypes = [_u16p, C.c_size_t, _u8p]
         L.ref_awgn_gtest_frames.restype = C.c_size_t
+        L.ref_demod_frames.argtypes = [_f32p, C.c_size_t, C.c_size_t, C.c_uint, C.c_int, C.c_uint,
+                                       C.c_int, C.c_float, _u16p, C.c_size_t, _u8p, _f32p, _f32p,
+                                       _i64p, C.c_int]
         for name, rt in [("ref_enc_h84", C.c_uint8), ("ref_enc_h74", C.c_uint8),
                          ("ref_enc_p54", C.c_uint8), ("ref_enc_p64", C.c_uint8)]:
             getattr(L, name).restype = rt

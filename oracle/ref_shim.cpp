@@ -6,7 +6,9 @@
 // copied from the reference: these wrappers only marshal plain pointers into the
 // reference's public API (include/lora_phy/phy.hpp:102-215, ChirpGenerator.hpp,
 // kissfft.hh, LoRaCodes.hpp) so that Python tests can call it through ctypes.
-// Available only in the build container (the reference does not exist on the GPU box).
+// Built only in the build container (the reference sources do not exist on the GPU
+// box); the built .so travels with the repo snapshot, where bench.py's cpu_baseline
+// times ref_demod_frames - the reference's own lora_demodulate - on the host cores.
 #include <lora_phy/phy.hpp>
 #include <lora_phy/ChirpGenerator.hpp>
 #include <lora_phy/LoRaCodes.hpp>
@@ -15,6 +17,7 @@
 #include <complex>
 #include <cstring>
 #include <random>
+#include <thread>
 #include <vector>
 
 using cpx = std::complex<float>;
@@ -225,6 +228,53 @@ size_t ref_awgn_gtest_frames(const unsigned* sfs, const unsigned* bws, int nprof
     }
   }
   return off;
+}
+
+
+// The reference's usage pattern (tests/e2e_chain_test.cpp:79-101) over F frames of
+// frame_len samples: optional caller-side dechirp with a genChirp down-chirp table,
+// then one lora_demodulate per frame with a caller-owned scratch buffer; `threads`
+// workers each own a workspace (the reference is reentrant per workspace).
+void ref_demod_frames(const float* iq, size_t frames, size_t frame_len, unsigned sf, int hann,
+                      unsigned osr, int dechirp, float bw_scale, uint16_t* out_syms,
+                      size_t sym_stride, uint8_t* out_sync, float* out_cfo, float* out_toff,
+                      int64_t* out_count, int threads) {
+  if (threads < 1) threads = 1;
+  auto worker = [&](int tid) {
+    auto* ws = new lora_phy::lora_demod_workspace();
+    std::vector<cpx> scratch(frame_len ? frame_len : 1), dech(dechirp ? frame_len : 0);
+    const size_t N = size_t(1) << sf, step = N * (osr ? osr : 1);
+    std::vector<cpx> down(dechirp ? step : 0);
+    if (dechirp) {
+      float ph = 0.0f;
+      genChirp(down.data(), (int)N, (int)(osr ? osr : 1), (int)step, 0.0f, true, 1.0f, ph, bw_scale);
+    }
+    lora_phy::lora_demod_init(ws, sf,
+                              hann ? lora_phy::window_type::window_hann
+                                   : lora_phy::window_type::window_none,
+                              scratch.data(), scratch.size());
+    for (size_t f = (size_t)tid; f < frames; f += (size_t)threads) {
+      const cpx* x = reinterpret_cast<const cpx*>(iq) + f * frame_len;
+      if (dechirp) {
+        for (size_t j = 0; j < frame_len; ++j) dech[j] = x[j] * down[j % step];
+        x = dech.data();
+      }
+      uint8_t sync = 0;
+      ws->metrics = lora_phy::lora_metrics{};
+      const size_t n = lora_phy::lora_demodulate(ws, x, frame_len, out_syms + f * sym_stride, osr,
+                                                 &sync);
+      if (out_sync) out_sync[f] = sync;
+      if (out_cfo) out_cfo[f] = ws->metrics.cfo;
+      if (out_toff) out_toff[f] = ws->metrics.time_offset;
+      if (out_count) out_count[f] = (int64_t)n;
+    }
+    lora_phy::lora_demod_free(ws);
+    delete ws;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(worker, t);
+  worker(0);
+  for (auto& th : pool) th.join();
 }
 
 }  // extern "C"
