@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_round.sh run into profiles/<round>/.
+
+  kernel_stats.md   per-kernel calls / avg / total duration from the rocprofv3
+                    --kernel-trace --stats database (split by grid size, so the SF7 and
+                    SF12 launches of a shared kernel are separate rows)
+  pmc.md            FETCH_SIZE / WRITE_SIZE per launch for our kernels
+  ../pmc_summary.json  HBM bytes per launch of the dominant (demod) kernel per workload,
+                    read by bench.py for roofline.traffic.  gfx950 correction
+                    (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes
+                    of a coalesced streaming read -> x2; WRITE_SIZE is exact.  The demod
+                    kernel's 8-byte-per-lane coalesced gathers calibrate the same way: x2
+                    FETCH_SIZE lands within 0.3% of the frames' IQ bytes (checked below).
+
+usage: prof_summary.py <gpurun_out/round> <profiles/rNN>
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sqlite3
+import sys
+
+
+def short(name: str) -> str:
+    m = re.search(r"(k_\w+(<[^>]*>)?)", name)
+    if m:
+        return m.group(1)
+    return name[:60]
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, grid_x, workgroup_x, duration, lds_size, vgpr_count, sgpr_count,"
+                     " scratch_size from kernels").fetchall()
+    agg = collections.OrderedDict()
+    for name, gx, wx, dur, lds, vgpr, sgpr, scratch in rows:
+        key = (short(name), gx // max(wx, 1))
+        a = agg.setdefault(key, {"calls": 0, "ns": 0.0, "lds": lds, "vgpr": vgpr, "sgpr": sgpr,
+                                 "scratch": scratch})
+        a["calls"] += 1
+        a["ns"] += float(dur)
+    return agg
+
+
+def pmc(dirpat):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(dirpat)):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            out[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(dst, exist_ok=True)
+    agg = kernel_stats(os.path.join(src, "kt", "run_results.db"))
+    lines = ["# rocprofv3 --kernel-trace --stats: `python bench.py --steps 10 --warmup 2 --no-cpu`",
+             "", "Durations from the rocprofv3 kernel trace (ns).  Workgroups = grid/workgroup size;",
+             "SF7 launches: 15,625 frames; SF12: 15,625 frames.", "",
+             "| kernel | workgroups | calls | avg us | total us | LDS B | VGPR | SGPR | scratch |",
+             "|---|---:|---:|---:|---:|---:|---:|---:|---:|"]
+    for (k, wg), a in sorted(agg.items(), key=lambda kv: -kv[1]["ns"]):
+        lines.append(f"| `{k}` | {wg} | {a['calls']} | {a['ns'] / a['calls'] / 1e3:.2f} | "
+                     f"{a['ns'] / 1e3:.1f} | {a['lds']} | {a['vgpr']} | {a['sgpr']} | {a['scratch']} |")
+    open(os.path.join(dst, "kernel_stats.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+    summary = {}
+    plines = ["# HBM counters per launch (rocprofv3 --pmc, one counter per pass)", "",
+              "FETCH_SIZE / WRITE_SIZE in KB as reported; `read B (x2)` applies the gfx950",
+              "correction from MI355X_MICROARCH.md (FETCH_SIZE = half the bytes of a coalesced read).", "",
+              "| workload | kernel | FETCH_SIZE KB | read B (x2) | WRITE_SIZE KB | HBM B/launch |",
+              "|---|---|---:|---:|---:|---:|"]
+    for wl, tag in (("sf7", "nosf12"), ("sf12", "sf12only")):
+        f = pmc(os.path.join(src, f"pmc_FETCH_SIZE{tag}", "run_counter_collection.csv"))
+        w = pmc(os.path.join(src, f"pmc_WRITE_SIZE{tag}", "run_counter_collection.csv"))
+        for k in f:
+            if not k.startswith("k_"):
+                continue
+            fk = sum(f[k]["FETCH_SIZE"]) / len(f[k]["FETCH_SIZE"])
+            wk = sum(w[k]["WRITE_SIZE"]) / len(w[k]["WRITE_SIZE"]) if k in w else 0.0
+            hbm = fk * 1024 * 2 + wk * 1024
+            plines.append(f"| {wl} | `{k}` | {fk:.0f} | {fk * 2048:.4g} | {wk:.0f} | {hbm:.4g} |")
+            if k.startswith("k_demod"):
+                summary[wl] = {"kernel": k, "fetch_size_kb": fk, "write_size_kb": wk,
+                               "hbm_bytes_per_launch": hbm}
+    sf = {"sf7": 7, "sf12": 12}
+    for wl, d in summary.items():
+        algo = 15625 * 64 * (8 * (1 << sf[wl]) + 2)
+        d["algorithmic_bytes_per_launch"] = algo
+        d["traffic_over_algorithmic"] = d["hbm_bytes_per_launch"] / algo
+        plines.append("")
+        plines.append(f"{wl}: demod HBM {d['hbm_bytes_per_launch']:.4g} B vs algorithmic {algo:.4g} B "
+                      f"-> {d['traffic_over_algorithmic']:.3f}x")
+    open(os.path.join(dst, "pmc.md"), "w").write("\n".join(plines) + "\n")
+    print("\n".join(plines))
+    json.dump(summary, open(os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_summary.json"), "w"),
+              indent=1)
+
+
+if __name__ == "__main__":
+    main()

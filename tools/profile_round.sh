@@ -16,7 +16,7 @@ tail -1 $OUT/smoke.log
 step bench
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 step kernel-trace
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run -- python bench.py --steps 10 --warmup 2 --no-cpu > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d $OUT/kt -o run -- python bench.py --steps 10 --warmup 2 --no-cpu > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
 for grp in FETCH_SIZE WRITE_SIZE; do
   for cfg in "--no-sf12" "--sf12-only"; do
     tag=$(echo "$grp$cfg" | tr -d '-')
