@@ -54,7 +54,7 @@ int set_error(int code, const std::string& msg) {
       return set_error(LORA_EIO, std::string(#expr) + ": " + hipGetErrorString(e_));      \
   } while (0)
 
-const float PI_F = float(M_PI);
+using lora::PI_F;
 
 // ---------------------------------------------------------------------------------
 // Host-side table generation (runs once per plan, on the host, with the reference's
@@ -823,7 +823,8 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
       hipLaunchKernelGGL(k_frame_max, dim3((unsigned)(nf * bpf)), dim3(256), 0, s, ac, bpf, chunk, mb);
     }
     ProfScope ps(plan, 1, s);
-    hipLaunchKernelGGL(k_estimate, dim3((unsigned)nf), dim3(256), sizeof(cf) * plan->N, s, ac);
+    if (!plan->use_fast || !lora::launch_est_fast(ac, nf, s))
+      hipLaunchKernelGGL(k_estimate, dim3((unsigned)nf), dim3(256), sizeof(cf) * plan->N, s, ac);
   };
   auto demod = [&](const KArgs& ac, int64_t nf, hipStream_t s) {
     const int64_t work = nf * per;

@@ -155,60 +155,38 @@ __device__ __forceinline__ void write_pass(cf* row, const cf* x, int l) {
   }
 }
 
-// MODE 0: LEGACY + fused dechirp, osr 1, no window (the benchmark configuration);
-// MODE 1: LEGACY on already-dechirped input, osr 1, no window (lora_demodulate's own
-//         contract); MODE 2: every other configuration, flags read at run time.
-// ABL: profiling-only ablation mask (LORA_MI355X_ABLATE; results are NOT valid):
-// 1 = identity rotation instead of sincosf, 2 = skip the pass-1 FFT stages, 4 = skip
-// the HBM loads.
-template <int SF, int MODE, int ABL = 0>
-__global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
-  using G = Geo<SF>;
-  constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1, SPW = G::SPW;
-  constexpr bool WL = G::WAVE_LOCAL;
-  constexpr bool DYN = MODE == 2;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  cf* rows = reinterpret_cast<cf*>(smem);
-  const int tid = threadIdx.x;
-  const int per = a.total - s0;
-  const int step = DYN ? a.step : N;
-  const int osr = DYN ? a.osr : 1;
-  const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
-  const bool dech = DYN ? (legacy && a.dechirp) : (MODE == 0);
-  const bool hann = DYN ? (a.hann != 0) : false;
+// ---- shared building blocks of the demod and estimate kernels --------------------
 
-  // ---- symbol of this lane: window base with the t_off rule (LoRaDemod.cpp:142-149)
-  // and rotation start phase (:151-152); every lane of the symbol computes it.
-  const int g = tid / T;  // slot
-  const int l = tid % T;  // lane within the symbol
-  const int64_t w = (int64_t)blockIdx.x * SPW + g;
-  const bool valid = w < work;
-  const int64_t wc = valid ? w : work - 1;  // clamp: invalid lanes mirror a valid symbol
-  const int64_t f = wc / per;
-  const int s = s0 + (int)(wc - f * per);
-  const FrameParams p = a.fp[f];
-  int64_t base = (int64_t)s * step;
-  int cg = 0;
-  if (p.t_off > 0) {
-    if (base + p.t_off + step <= a.frame_len) {
-      base += p.t_off;
-      cg = p.t_off;
+// Window base of symbol s with the t_off rule (LoRaDemod.cpp:142-149): `base` is the
+// sample offset in the frame, `cg` the phase of the caller-side dechirp table there.
+__device__ __forceinline__ void sym_base(int s, int step, int64_t frame_len, int t_off,
+                                         int64_t& base, int& cg) {
+  base = (int64_t)s * step;
+  cg = 0;
+  if (t_off > 0) {
+    if (base + t_off + step <= frame_len) {
+      base += t_off;
+      cg = t_off;
     }
-  } else if (p.t_off < 0) {
-    const int64_t off = -(int64_t)p.t_off;
+  } else if (t_off < 0) {
+    const int64_t off = -(int64_t)t_off;
     if (off <= base) {
       base -= off;
       cg = step - (int)off;
     }
   }
-  const cf* __restrict__ x = a.iq + f * a.frame_stride + base;
-  const float start = p.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)p.t_off / (float)osr);
-  const float rate = p.rate;
-  // LoRaDemod.cpp:68-77: scale is 1.0f when the frame is not rescaled (x*1.0f == x).
-  const float scale = (legacy && p.scaled) ? p.scale : 1.0f;
+}
 
-  // ---- pass 1: gather 16 points (stride T), dechirp / scale / rotate / window ----
-  cf in[P];
+// Gather the lane's P points x[(l + T*q)*osr] of one symbol window straight from HBM
+// and apply what precedes the rotation: KIND 0 raw (API estimate, phy.cpp:91-99),
+// KIND 1 LEGACY (caller dechirp, e2e_chain_test.cpp:88-93, then normalisation,
+// LoRaDemod.cpp:68-77), KIND 2 API down-chirp (phy.cpp:216-225).
+template <int SF, int ABL>
+__device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restrict__ x, int l,
+                                              int osr, int step, int cg, int kind, bool dech,
+                                              float scale, cf* in) {
+  using G = Geo<SF>;
+  constexpr int T = G::T, P = G::P;
 #pragma unroll
   for (int q = 0; q < P; ++q) {
     const int i = l + T * q;
@@ -217,10 +195,10 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
     else
       in[q] = x[(int64_t)i * osr];
   }
-  if (!legacy) {
+  if (kind == 2) {
 #pragma unroll
     for (int q = 0; q < P; ++q) in[q] = cmul(in[q], a.down1[l + T * q]);
-  } else {
+  } else if (kind == 1) {
     if (dech) {
 #pragma unroll
       for (int q = 0; q < P; ++q) {
@@ -232,14 +210,28 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
 #pragma unroll
     for (int q = 0; q < P; ++q) in[q] = cscale(in[q], scale);
   }
+}
+
+// CFO rotation (glibc-faithful sincosf, LoRaDemod.cpp:151-157) when ROT, window
+// (:158-160), and placement in pass-1 leaf order.
+template <int SF, bool ROT, int ABL>
+__device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, float rate,
+                                             bool hann, const float* __restrict__ win, int l) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
+  if (!ROT || (ABL & 1)) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      cf v = in[q];
+      if (hann && !(ABL & 1)) v = cscale(v, win[l + T * q]);
+      z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
+    }
+    return;
+  }
   // The rotation phase is monotone in i, so the symbol's |ph| range is bounded by its
   // two end points; the branch-free sincosf covers |ph| < 120 (lora_libm.h).
   const bool sym_fast = lm_sincosf_fast_ok(start) && lm_sincosf_fast_ok(start + rate * (float)(N - 1));
-  cf z[P];
-  if (ABL & 1) {
-#pragma unroll
-    for (int q = 0; q < P; ++q) z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = in[q];
-  } else if (__all(sym_fast)) {
+  if (__all(sym_fast)) {
     constexpr int K = 4;
 #pragma unroll
     for (int q0 = 0; q0 < P; q0 += K) {
@@ -251,7 +243,7 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
       for (int k = 0; k < K; ++k) {
         const int q = q0 + k;
         cf v = cmul(in[q], cf{cs[k], sn[k]});
-        if (hann) v = cscale(v, a.win[l + T * q]);
+        if (hann) v = cscale(v, win[l + T * q]);
         z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
       }
     }
@@ -262,15 +254,24 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
       float sn, cs;
       lm_sincosf(ph, &sn, &cs);
       cf v = cmul(in[q], cf{cs, sn});
-      if (hann) v = cscale(v, a.win[l + T * q]);
+      if (hann) v = cscale(v, win[l + T * q]);
       z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
     }
   }
+}
+
+// FFT of the symbol held as pass-1 inputs in z (T lanes x P points) and the lane's
+// argmax key.  KEEP: leave the spectrum in natural order in `row` (padded address
+// paddr(bin)) for the estimate's neighbour bins; NPASS == 1 keeps it in z.
+template <int SF, bool KEEP, int ABL>
+__device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
+  constexpr bool WL = G::WAVE_LOCAL;
   if (!(ABL & 2)) {
 #pragma unroll
     for (int h = 0; h < G::G1; ++h) pass_regs<R1, G::R2FIRST, N, 1>(z + h * R1, 0, a.tw);
   }
-
   uint64_t key = 0;
   if constexpr (G::NPASS == 1) {
     float best = 0.0f;
@@ -285,7 +286,6 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
     }
     key = ((uint64_t)__float_as_uint(best) << 32) | (uint32_t)(~bi);
   } else {
-    cf* row = rows + (size_t)g * rowc;
     int c[G::G1];
 #pragma unroll
     for (int h = 0; h < G::G1; ++h) c[h] = (int)(a.rev[l + T * h] >> G::LOGR1);
@@ -294,6 +294,8 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
 #pragma unroll
       for (int u = 0; u < R1; ++u) row[paddr<G::LOGR1>(c[h] * R1 + u)] = z[h * R1 + u];
     block_sync<WL>();
+    constexpr int RL = G::NPASS == 2 ? G::RA : G::RB;   // last pass span
+    constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
     if constexpr (G::NPASS == 2) {
       pass_lds<G::RA, N, G::MA_A, G::LOGR1, T, P, true>(row, z, l, a.tw, key);
     } else {
@@ -303,13 +305,26 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
       block_sync<WL>();
       pass_lds<G::RB, N, G::MA_B, G::LOGR1, T, P, true>(row, z, l, a.tw, key);
     }
+    if constexpr (KEEP) {
+      // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)
+      block_sync<WL>();
+#pragma unroll
+      for (int gg = 0; gg < P / RL; ++gg)
+#pragma unroll
+        for (int u = 0; u < RL; ++u) row[paddr<G::LOGR1>(l + T * gg + ML * u)] = z[gg * RL + u];
+      block_sync<WL>();
+    }
   }
+  return key;
+}
 
-  // ---- argmax across the T lanes of the symbol ----
+// Argmax key over the T lanes of a symbol; every lane of the symbol gets the result.
+template <int SF>
+__device__ __forceinline__ uint64_t symbol_key(uint64_t key, int tid, uint64_t* red) {
+  constexpr int T = Geo<SF>::T;
   if constexpr (T <= 64) {
-    key = group_max(key, T);
+    return group_max(key, T);
   } else {
-    __shared__ uint64_t red[4];
     key = group_max(key, 64);
     __syncthreads();
     if ((tid & 63) == 0) red[tid >> 6] = key;
@@ -319,18 +334,233 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
     uint64_t r = red[wb];
 #pragma unroll
     for (int q = 1; q < WPS; ++q) r = umax64(r, red[wb + q]);
-    key = r;
+    return r;
   }
+}
+
+// MODE 0: LEGACY + fused dechirp, osr 1, no window (the benchmark configuration);
+// MODE 1: LEGACY on already-dechirped input, osr 1, no window (lora_demodulate's own
+//         contract); MODE 2: every other configuration, flags read at run time.
+// ABL: profiling-only ablation mask (LORA_MI355X_ABLATE; results are NOT valid):
+// 1 = identity rotation instead of sincosf, 2 = skip the pass-1 FFT stages, 4 = skip
+// the HBM loads.
+template <int SF, int MODE, int ABL = 0>
+__global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
+  constexpr bool DYN = MODE == 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint64_t red[4];
+  cf* rows = reinterpret_cast<cf*>(smem);
+  const int tid = threadIdx.x;
+  const int per = a.total - s0;
+  const int step = DYN ? a.step : N;
+  const int osr = DYN ? a.osr : 1;
+  const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
+  const bool dech = DYN ? (legacy && a.dechirp) : (MODE == 0);
+  const bool hann = DYN ? (a.hann != 0) : false;
+
+  const int g = tid / T;  // slot
+  const int l = tid % T;  // lane within the symbol
+  const int64_t w = (int64_t)blockIdx.x * SPW + g;
+  const bool valid = w < work;
+  const int64_t wc = valid ? w : work - 1;  // clamp: invalid lanes mirror a valid symbol
+  const int64_t f = wc / per;
+  const int s = s0 + (int)(wc - f * per);
+  const FrameParams p = a.fp[f];
+  int64_t base;
+  int cg;
+  sym_base(s, step, a.frame_len, p.t_off, base, cg);
+  const cf* __restrict__ x = a.iq + f * a.frame_stride + base;
+  const float start = p.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)p.t_off / (float)osr);
+  // LoRaDemod.cpp:68-77: scale is 1.0f when the frame is not rescaled (x*1.0f == x).
+  const float scale = (legacy && p.scaled) ? p.scale : 1.0f;
+
+  cf in[P], z[P];
+  gather_points<SF, ABL>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, scale, in);
+  rotate_place<SF, true, ABL>(in, z, start, p.rate, hann, a.win, l);
+  uint64_t key = fft_key<SF, false, ABL>(z, rows + (size_t)g * rowc, l, a);
+  key = symbol_key<SF>(key, tid, red);
   if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + (s - s0)] = (uint16_t)key_index(key);
+}
+
+// Offset estimate + sync symbols, one T-lane group per frame (LoRaDemod.cpp:79-135,
+// 165-168, 177-192; phy.cpp:78-145, 228-237), for frames with >= 2 whole symbols.
+// Per frame: for each of symbols 0,1 and osr phase t, the FFT of the (dechirped,
+// normalised | raw) windowed samples, the detector tail on the winning bin (power,
+// fractional index, LoRaDetector.hpp:60-71) and the phase of that bin; lane 0 keeps
+// the estimator state.  Then symbols 0/1 are demodulated with the estimated offsets
+// exactly as k_demod_fast does for the data symbols, giving the sync word.
+template <int SF, int MODE>
+__global__ void __launch_bounds__(256) k_est_fast(KArgs a, int64_t frames, int rowc) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P;
+  constexpr int SPB = (T >= 64 ? 256 : 64) / T;  // frames per block (block = max(T, 64))
+  constexpr bool DYN = MODE == 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint64_t red[4];
+  __shared__ FrameParams sp[SPB];
+  const int tid = threadIdx.x;
+  const int step = DYN ? a.step : N;
+  const int osr = DYN ? a.osr : 1;
+  const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
+  const bool dech = DYN ? (legacy && a.dechirp) : (MODE == 0);
+  const bool hann = DYN ? (a.hann != 0) : false;
+  const int g = tid / T;
+  const int l = tid % T;
+  const int64_t f0 = (int64_t)blockIdx.x * SPB + g;
+  const bool valid = f0 < frames;
+  const int64_t f = valid ? f0 : frames - 1;
+  const cf* __restrict__ x = a.iq + f * a.frame_stride;
+  cf* row = reinterpret_cast<cf*>(smem) + (size_t)g * rowc;
+  const float maxv = legacy ? __uint_as_float(a.maxbits[f]) : 0.0f;
+  const int scaled = maxv > 1.0f;
+  const float scale = scaled ? 1.0f / maxv : 1.0f;
+
+  float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
+  bool have_prev = false;
+  unsigned sum_t = 0;
+  cf in[P], z[P];
+  for (int s = 0; s < 2; ++s) {
+    float best_p = -1e30f, best_fi = 0.0f;
+    uint32_t best_idx = 0;
+    unsigned best_t = 0;
+    cf best_bin = {0.0f, 0.0f};
+    for (int t = 0; t < osr; ++t) {
+      gather_points<SF, 0>(a, x + (int64_t)s * step + t, l, osr, step, t, legacy ? 1 : 0, dech,
+                           scale, in);
+      rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
+      uint64_t key = fft_key<SF, true, 0>(z, row, l, a);
+      key = symbol_key<SF>(key, tid, red);
+      if (l == 0) {
+        const uint32_t idx = key_index(key);
+        const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
+        cf L, R, B;
+        if constexpr (G::NPASS == 1) {
+          L = R = B = cf{0.0f, 0.0f};
+#pragma unroll
+          for (int u = 0; u < N; ++u) {
+            if ((uint32_t)u == im1) L = z[u];
+            if ((uint32_t)u == ip1) R = z[u];
+            if ((uint32_t)u == idx) B = z[u];
+          }
+        } else {
+          L = row[paddr<G::LOGR1>((int)im1)];
+          R = row[paddr<G::LOGR1>((int)ip1)];
+          B = row[paddr<G::LOGR1>((int)idx)];
+        }
+        float pw, fi;
+        detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
+        if (pw > best_p || (legacy && pw == best_p && idx < best_idx)) {
+          best_p = pw;
+          best_idx = idx;
+          best_fi = fi;
+          best_t = (unsigned)t;
+          best_bin = B;
+        }
+      }
+      block_sync<G::WAVE_LOCAL>();  // row is rewritten by the next transform
+    }
+    if (l == 0) {
+      sum_t += best_t;
+      sum_index += (float)best_idx + best_fi;
+      const float phase = lm_atan2f(best_bin.im, best_bin.re);
+      if (have_prev) {
+        float d = phase - prev_phase;
+        while (d > PI_F) d -= 2.0f * PI_F;
+        while (d < -PI_F) d += 2.0f * PI_F;
+        phase_diff += d;
+      }
+      prev_phase = phase;
+      have_prev = true;
+    }
+  }
+  if (l == 0) {
+    const float avg_index = sum_index / 2.0f;
+    const float cfo_coarse = avg_index / (float)N;
+    const float cfo_fine = (phase_diff / 1.0f) / (2.0f * PI_F * (float)N);
+    const float cfo = cfo_coarse + cfo_fine;
+    const float frac = avg_index - floorf(avg_index + 0.5f);
+    const float avg_t = (float)sum_t / 2.0f;
+    const float toff = avg_t - frac * (float)N * (float)osr;
+    FrameParams q;
+    q.cfo = cfo;
+    q.toff = toff;
+    q.t_off = (int)roundf(toff);
+    q.rate = -2.0f * PI_F * cfo / (float)N;
+    q.scale = scale;
+    q.scaled = scaled;
+    q.pad0 = q.pad1 = 0;
+    sp[g] = q;
+    if (valid) {
+      a.fp[f] = q;
+      if (a.cfo) a.cfo[f] = cfo;
+      if (a.toff) a.toff[f] = toff;
+      if (a.max_amp) a.max_amp[f] = maxv;
+    }
+  }
+  block_sync<G::WAVE_LOCAL>();
+  const FrameParams q = sp[g];
+  uint32_t sw[2];
+  for (int s = 0; s < 2; ++s) {
+    int64_t base;
+    int cg;
+    sym_base(s, step, a.frame_len, q.t_off, base, cg);
+    const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
+    gather_points<SF, 0>(a, x + base, l, osr, step, cg, legacy ? 1 : 2, dech,
+                         (legacy && q.scaled) ? q.scale : 1.0f, in);
+    rotate_place<SF, true, 0>(in, z, start, q.rate, hann, a.win, l);
+    uint64_t key = fft_key<SF, false, 0>(z, row, l, a);
+    key = symbol_key<SF>(key, tid, red);
+    sw[s] = key_index(key);
+    block_sync<G::WAVE_LOCAL>();
+  }
+  if (l == 0 && valid && a.sync) {
+    const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
+    a.sync[f] = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
+  }
+}
+
+template <int SF>
+int row_complex() {
+  using G = Geo<SF>;
+  int rowc = G::N + (G::N >> G::LOGR1);  // padded transpose image
+  // rows 16-byte aligned and staggered by 16 banks (rowc = 8 mod 32 complex) so the
+  // symbols of one wave hit different banks in the strided pass-1 gather
+  while (rowc % 32 != 8) ++rowc;
+  return rowc;
+}
+
+template <int SF, int MODE>
+bool launch_est_mode(const KArgs& a, int64_t frames, hipStream_t st) {
+  using G = Geo<SF>;
+  constexpr int T = G::T;
+  constexpr int BLOCK = T >= 64 ? 256 : 64;
+  constexpr int SPB = BLOCK / T;
+  const int rowc = row_complex<SF>();
+  const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * (size_t)SPB * rowc;
+  if (lds > 160 * 1024) return false;
+  if (lds > 64 * 1024)
+    if (hipFuncSetAttribute((const void*)k_est_fast<SF, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return false;
+  const int64_t grid = (frames + SPB - 1) / SPB;
+  hipLaunchKernelGGL((k_est_fast<SF, MODE>), dim3((unsigned)grid), dim3(BLOCK), lds, st, a, frames, rowc);
+  return true;
+}
+
+template <int SF>
+bool launch_est_sf(const KArgs& a, int64_t frames, hipStream_t st) {
+  const bool simple = a.mode == LORA_MODE_LEGACY && a.osr == 1 && !a.hann;
+  if (simple && a.dechirp) return launch_est_mode<SF, 0>(a, frames, st);
+  if (simple) return launch_est_mode<SF, 1>(a, frames, st);
+  return launch_est_mode<SF, 2>(a, frames, st);
 }
 
 template <int SF, int MODE, int ABL = 0>
 bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   using G = Geo<SF>;
-  int rowc = G::N + (G::N >> G::LOGR1);                  // padded transpose image
-  // rows 16-byte aligned and staggered by 16 banks (rowc = 8 mod 32 complex) so the
-  // symbols of one wave hit different banks in the strided pass-1 gather
-  while (rowc % 32 != 8) ++rowc;
+  const int rowc = row_complex<SF>();
   const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * (size_t)G::SPW * rowc;
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
@@ -364,6 +594,24 @@ bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
 }
 
 }  // namespace
+
+bool launch_est_fast(const KArgs& a, int64_t frames, hipStream_t st) {
+  if (a.total < 2 || a.est_only) return false;
+  switch (a.sf) {
+    case 2: return launch_est_sf<2>(a, frames, st);
+    case 3: return launch_est_sf<3>(a, frames, st);
+    case 4: return launch_est_sf<4>(a, frames, st);
+    case 5: return launch_est_sf<5>(a, frames, st);
+    case 6: return launch_est_sf<6>(a, frames, st);
+    case 7: return launch_est_sf<7>(a, frames, st);
+    case 8: return launch_est_sf<8>(a, frames, st);
+    case 9: return launch_est_sf<9>(a, frames, st);
+    case 10: return launch_est_sf<10>(a, frames, st);
+    case 11: return launch_est_sf<11>(a, frames, st);
+    case 12: return launch_est_sf<12>(a, frames, st);
+    default: return false;
+  }
+}
 
 bool launch_demod_fast(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   switch (a.sf) {

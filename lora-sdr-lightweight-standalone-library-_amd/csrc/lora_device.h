@@ -15,6 +15,9 @@
 
 namespace lora {
 
+// float(M_PI), the reference's `float(M_PI)` (phy.cpp:40, LoRaDemod.cpp)
+constexpr float PI_F = 3.14159265358979323846f;
+
 struct cf {
   float re, im;
 };

@@ -30,4 +30,8 @@ struct KArgs {
 // Returns false if the configuration is not covered (caller uses the generic kernel).
 bool launch_demod_fast(const KArgs& a, int s0, int64_t work, hipStream_t st);
 
+// Offset estimate + sync symbols with the same FFT machinery, one lane group per frame
+// (frames with >= 2 whole symbols; false = not covered, use k_estimate).
+bool launch_est_fast(const KArgs& a, int64_t frames, hipStream_t st);
+
 }  // namespace lora
