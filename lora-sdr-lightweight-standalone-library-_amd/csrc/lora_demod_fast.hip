@@ -238,7 +238,7 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
       float ph[K], sn[K], cs[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) ph[k] = start + rate * (float)(l + T * (q0 + k));
-      lm_sincosf_fast_k<K>(ph, sn, cs);
+      lm_sincosf_fast_k_nz<K>(ph, sn, cs);  // argmax-only: sign of a zero sine is immaterial
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int q = q0 + k;

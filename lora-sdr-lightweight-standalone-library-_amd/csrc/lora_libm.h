@@ -237,6 +237,52 @@ LM_FN void lm_sincosf_fast_k(const float* y, float* sinp, float* cosp) {
   }
 }
 
+// lm_sincosf_fast_k for callers that only need the rotation's magnitude-relevant
+// bits (the demodulator's argmax): identical except that sin(-0) may come out +0
+// (glibc returns -0).  A zero's sign never changes |X|^2 of any bin, so symbol
+// indices are unaffected.  The quadrant sign of the reduced argument is applied by
+// flipping its sign bit instead of a select.
+template <int K>
+LM_FN void lm_sincosf_fast_k_nz(const float* y, float* sinp, float* cosp) {
+  double xs[K], x2[K], x3[K], x4[K], x5[K], x6[K];
+  int n[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double x = (double)y[k];
+    n[k] = (((int32_t)(x * LM_SC_HPI_INV)) + 0x800000) >> 24;
+    const double xr = lm_fma(-(double)n[k], LM_SC_HPI, x);
+    const uint64_t flip = (uint64_t)((uint32_t)(n[k] ^ (n[k] >> 1)) & 1u) << 63;
+    xs[k] = lm_asdouble(lm_asuint64(xr) ^ flip);  // sign[nq & 3] = {1,-1,-1,1}
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    x2[k] = xs[k] * xs[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    x3[k] = x2[k] * xs[k];
+    x4[k] = x2[k] * x2[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    x5[k] = x2[k] * x3[k];
+    x6[k] = x2[k] * x4[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double s1 = lm_fma(x2[k], LM_SC_S3, LM_SC_S2);
+    const double c2 = lm_fma(x2[k], LM_SC_C4, LM_SC_C3);
+    const double c1 = lm_fma(x2[k], LM_SC_C1, LM_SC_C0);
+    const double sp = lm_fma(x3[k], LM_SC_S1, xs[k]);
+    const double cp = lm_fma(x4[k], LM_SC_C2, c1);
+    const float sf = (float)lm_fma(s1, x5[k], sp);
+    float cf = (float)lm_fma(c2, x6[k], cp);
+    if (n[k] & 2) cf = -cf;
+    sinp[k] = (n[k] & 1) ? cf : sf;
+    cosp[k] = (n[k] & 1) ? sf : cf;
+  }
+}
+
 // True when lm_sincosf_fast is exact for y.
 LM_FN int lm_sincosf_fast_ok(float y) { return lm_abstop12(y) < 0x42fu; }
 
