@@ -122,12 +122,23 @@ def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=
     }
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=2.0):
     """The reference's own lora_demodulate (oracle/_ref, compiled from the reference's
     sources, travels with the snapshot) on `threads` host cores over a bounded sample of
     the same frames; falls back to the restatement (oracle/lora_oracle.cpp) if absent.
-    Sample: whole passes over the first `max_frames` frames until `time_budget_s` wall
-    seconds have elapsed (~30 CPU-seconds at 16 threads)."""
+    Reported `value`: all threads, caller-side dechirp + lora_demodulate (the GPU
+    workload).  Also: one core, and demod only (input dechirped beforehand), per
+    SURVEY.md 8d.  Each leg: whole passes over the sample until `time_budget_s`."""
     from oracle.pyoracle import Oracle, Reference
 
     if Reference.available():
@@ -136,19 +147,28 @@ def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=2.0):
         impl, kind, what = Oracle(), "port", "restatement oracle/lora_oracle.cpp"
     F = min(iq_dev.shape[0], max_frames)
     x = iq_dev[:F].cpu().numpy()
-    impl.demod_frames(x[: min(F, 4 * threads)], sf, 1, False, dechirp=True, threads=threads)  # warm
-    t0 = time.perf_counter()
-    done = 0
-    while True:
-        impl.demod_frames(x, sf, 1, False, dechirp=True, threads=threads)
-        done += F
-        if time.perf_counter() - t0 > time_budget_s:
-            break
-    dt = time.perf_counter() - t0
-    rate = done * data_syms / dt / 1e6
-    return {"value": rate, "unit": "Msymbols/s", "cores": threads, "kind": kind,
+
+    def rate(xs, nthreads, dechirp):
+        impl.demod_frames(xs[: min(len(xs), 4 * nthreads)], sf, 1, False, dechirp=dechirp, threads=nthreads)
+        t0 = time.perf_counter()
+        done = 0
+        while True:
+            impl.demod_frames(xs, sf, 1, False, dechirp=dechirp, threads=nthreads)
+            done += len(xs)
+            if time.perf_counter() - t0 > time_budget_s:
+                break
+        dt = time.perf_counter() - t0
+        return done * data_syms / dt / 1e6, done, dt
+
+    all_rate, done, dt = rate(x, threads, True)
+    one_rate, _, _ = rate(x[: max(1, F // max(threads, 1))], 1, True)
+    xd = Oracle().dechirp(x.reshape(-1), sf).reshape(x.shape)  # same fp32 products as the caller loop
+    demod_only, _, _ = rate(xd, threads, False)
+    return {"value": all_rate, "unit": "Msymbols/s", "cores": threads, "kind": kind,
+            "single_core": one_rate, "demod_only_all_cores": demod_only, "cpu_model": _cpu_model(),
             "sample": f"{done} frames of the SF{sf} bench batch ({data_syms}+2 symbols each), "
-                      f"caller-side dechirp + {what}, {threads} threads, {dt:.2f} s"}
+                      f"caller-side dechirp + {what}, {threads} threads, {dt:.2f} s; single_core: same "
+                      f"on 1 thread; demod_only: input dechirped beforehand"}
 
 
 def load_pmc(workload):

@@ -61,6 +61,12 @@ extern "C" {
  *   number (>= 2) of symbols. */
 #define LORA_MODE_LEGACY 0
 #define LORA_MODE_API 1
+/* RAW: the detector primitive alone - per whole symbol: (dechirp) -> (window) ->
+ *   2^SF FFT -> lowest-index argmax |X|^2 (LoRaDetector.hpp:39-58), no normalisation,
+ *   no offset estimate, no rotation, every symbol output (no sync word: sync, cfo,
+ *   time_offset, max_amp are written as 0).  This is the demodulator of the
+ *   reference's Python AWGN sweep (tests/awgn_sweep.py:262-265). */
+#define LORA_MODE_RAW 2
 
 typedef struct lora_demod_plan lora_demod_plan;
 
@@ -69,7 +75,7 @@ typedef struct {
   unsigned osr;   /* oversampling ratio >= 1 (0 is treated as 1, phy.cpp:32) */
   unsigned bw_hz; /* 125000, 250000 or 500000 (phy.hpp:37-41) */
   int window;     /* LORA_WINDOW_* */
-  int dechirp;    /* LEGACY only: 1 = input is raw IQ, multiply sample j of each frame
+  int dechirp;    /* LEGACY / RAW: 1 = input is raw IQ, multiply sample j of each frame
                      by genChirp(N, osr, N*osr, down)[j mod N*osr] first
                      (e2e_chain_test.cpp:85-93); 0 = input already dechirped */
   int mode;       /* LORA_MODE_* */

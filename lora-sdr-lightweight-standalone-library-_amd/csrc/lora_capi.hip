@@ -150,10 +150,15 @@ __device__ __forceinline__ cf symbol_point(const KArgs& a, const cf* __restrict_
   }
   const float start = p.rate * ((float)((uint32_t)s * (uint32_t)a.N) +
                                 (float)p.t_off / (float)a.osr);
+  const int64_t j = base + (int64_t)i * a.osr;
+  if (a.mode == LORA_MODE_RAW) {  // detector only: (dechirp) -> (window)
+    cf v = load_legacy(x, j, a.down, a.step, a.dechirp, 0, 1.0f);
+    if (a.hann) v = lora::cscale(v, a.win[i]);
+    return v;
+  }
   const float ph = start + p.rate * (float)i;
   float sn, cs;
   lm_sincosf(ph, &sn, &cs);
-  const int64_t j = base + (int64_t)i * a.osr;
   cf v;
   if (a.mode == LORA_MODE_API) {
     v = lora::cmul(lora::cmul(x[j], a.down1[i]), cf{cs, sn});
@@ -400,7 +405,8 @@ __global__ void __launch_bounds__(256) k_demod(KArgs a, int G, int s0, int64_t w
     if (w < work) {
       const int64_t f = w / per;
       const int s = s0 + (int)(w - f * per);
-      const lora::FrameParams p = a.fp[f];
+      const lora::FrameParams p =
+          a.mode == LORA_MODE_RAW ? lora::FrameParams{0.0f, 0.0f, 0.0f, 1.0f, 0, 0, 0, 0} : a.fp[f];
       v = symbol_point(a, a.iq + f * a.frame_stride, p, s, i);
     }
     A[g * N + a.rev[i]] = v;
@@ -598,7 +604,8 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   if (!bw_ok(p.bw_hz)) return set_error(LORA_EINVAL, "bw_hz must be 125000, 250000 or 500000");
   if (p.window != LORA_WINDOW_NONE && p.window != LORA_WINDOW_HANN)
     return set_error(LORA_EINVAL, "bad window");
-  if (p.mode != LORA_MODE_LEGACY && p.mode != LORA_MODE_API) return set_error(LORA_EINVAL, "bad mode");
+  if (p.mode != LORA_MODE_LEGACY && p.mode != LORA_MODE_API && p.mode != LORA_MODE_RAW)
+    return set_error(LORA_EINVAL, "bad mode");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (p.device < 0 || p.device >= ndev) return set_error(LORA_EINVAL, "bad device ordinal");
@@ -742,6 +749,7 @@ int64_t lora_demod_symbols_per_frame(const lora_demod_plan* plan, int64_t frame_
     if (total < 2) return set_error(LORA_EINVAL, "API mode: frame needs >= 2 symbols");  // phy.cpp:188
     return total - 2;
   }
+  if (plan->prm.mode == LORA_MODE_RAW) return total;
   return total >= 2 ? total - 2 : total;  // LoRaDemod.cpp:194
 }
 
@@ -785,8 +793,8 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.step = plan->step;
   a.total = (int)total;
   a.mode = p.mode;
-  a.have_sync = (p.mode == LORA_MODE_API) ? 1 : (total >= 2 ? 1 : 0);
-  a.dechirp = (p.mode == LORA_MODE_LEGACY && p.dechirp) ? 1 : 0;
+  a.have_sync = (p.mode == LORA_MODE_API) ? 1 : (p.mode == LORA_MODE_LEGACY && total >= 2 ? 1 : 0);
+  a.dechirp = (p.mode != LORA_MODE_API && p.dechirp) ? 1 : 0;
   a.hann = p.window == LORA_WINDOW_HANN;
   a.power_scale = plan->power_scale;
   a.tw = plan->tw;
@@ -850,7 +858,16 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   };
   const int nchunks = (int)std::min<int64_t>(plan->max_chunks, frames / 1024);
   int rc = LORA_OK;
-  if (nchunks <= 1) {
+  if (p.mode == LORA_MODE_RAW) {
+    // detector only: per-frame outputs are defined as 0
+    hipError_t e = hipSuccess;
+    if (a.sync) e = hipMemsetAsync(a.sync, 0, (size_t)frames, st);
+    if (a.cfo && e == hipSuccess) e = hipMemsetAsync(a.cfo, 0, sizeof(float) * (size_t)frames, st);
+    if (a.toff && e == hipSuccess) e = hipMemsetAsync(a.toff, 0, sizeof(float) * (size_t)frames, st);
+    if (a.max_amp && e == hipSuccess) e = hipMemsetAsync(a.max_amp, 0, sizeof(float) * (size_t)frames, st);
+    if (e != hipSuccess) rc = set_error(LORA_EIO, "hipMemsetAsync failed");
+    if (rc == LORA_OK) demod(a, frames, st);
+  } else if (nchunks <= 1) {
     if (p.mode == LORA_MODE_LEGACY && hipMemsetAsync(maxbits, 0, ws_counter_bytes(frames), st) != hipSuccess)
       rc = set_error(LORA_EIO, "hipMemsetAsync failed");
     if (rc == LORA_OK) {

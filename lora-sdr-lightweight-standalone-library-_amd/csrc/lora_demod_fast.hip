@@ -340,7 +340,8 @@ __device__ __forceinline__ uint64_t symbol_key(uint64_t key, int tid, uint64_t* 
 
 // MODE 0: LEGACY + fused dechirp, osr 1, no window (the benchmark configuration);
 // MODE 1: LEGACY on already-dechirped input, osr 1, no window (lora_demodulate's own
-//         contract); MODE 2: every other configuration, flags read at run time.
+//         contract); MODE 2: every other LEGACY / API configuration, flags read at run
+//         time; MODE 3: RAW (detector only: no normalisation, estimate or rotation).
 // ABL: profiling-only ablation mask (LORA_MI355X_ABLATE; results are NOT valid):
 // 1 = identity rotation instead of sincosf, 2 = skip the pass-1 FFT stages, 4 = skip
 // the HBM loads.
@@ -348,7 +349,8 @@ template <int SF, int MODE, int ABL = 0>
 __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
-  constexpr bool DYN = MODE == 2;
+  constexpr bool RAW = MODE == 3;
+  constexpr bool DYN = MODE >= 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint64_t red[4];
   cf* rows = reinterpret_cast<cf*>(smem);
@@ -356,7 +358,7 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
   const int per = a.total - s0;
   const int step = DYN ? a.step : N;
   const int osr = DYN ? a.osr : 1;
-  const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
+  const bool legacy = RAW ? true : DYN ? a.mode != LORA_MODE_API : true;
   const bool dech = DYN ? (legacy && a.dechirp) : (MODE == 0);
   const bool hann = DYN ? (a.hann != 0) : false;
 
@@ -367,7 +369,7 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
   const int64_t wc = valid ? w : work - 1;  // clamp: invalid lanes mirror a valid symbol
   const int64_t f = wc / per;
   const int s = s0 + (int)(wc - f * per);
-  const FrameParams p = a.fp[f];
+  const FrameParams p = RAW ? FrameParams{0.0f, 0.0f, 0.0f, 1.0f, 0, 0, 0, 0} : a.fp[f];
   int64_t base;
   int cg;
   sym_base(s, step, a.frame_len, p.t_off, base, cg);
@@ -378,7 +380,7 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
 
   cf in[P], z[P];
   gather_points<SF, ABL>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, scale, in);
-  rotate_place<SF, true, ABL>(in, z, start, p.rate, hann, a.win, l);
+  rotate_place<SF, !RAW, ABL>(in, z, start, p.rate, hann, a.win, l);
   uint64_t key = fft_key<SF, false, ABL>(z, rows + (size_t)g * rowc, l, a);
   key = symbol_key<SF>(key, tid, red);
   if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + (s - s0)] = (uint16_t)key_index(key);
@@ -588,6 +590,7 @@ bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
       }
     }
   }
+  if (a.mode == LORA_MODE_RAW) return launch_mode<SF, 3>(a, s0, work, st);
   if (simple && a.dechirp) return launch_mode<SF, 0>(a, s0, work, st);
   if (simple) return launch_mode<SF, 1>(a, s0, work, st);
   return launch_mode<SF, 2>(a, s0, work, st);
@@ -596,7 +599,7 @@ bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
 }  // namespace
 
 bool launch_est_fast(const KArgs& a, int64_t frames, hipStream_t st) {
-  if (a.total < 2 || a.est_only) return false;
+  if (a.total < 2 || a.est_only || a.mode == LORA_MODE_RAW) return false;
   switch (a.sf) {
     case 2: return launch_est_sf<2>(a, frames, st);
     case 3: return launch_est_sf<3>(a, frames, st);

@@ -21,6 +21,7 @@ LORA_WINDOW_NONE = 0
 LORA_WINDOW_HANN = 1
 LORA_MODE_LEGACY = 0
 LORA_MODE_API = 1
+LORA_MODE_RAW = 2
 
 # Every symbol include/lora_mi355x.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (

@@ -17,7 +17,7 @@ from . import _capi
 
 _WINDOWS = {"none": _capi.LORA_WINDOW_NONE, "hann": _capi.LORA_WINDOW_HANN,
             None: _capi.LORA_WINDOW_NONE, 0: _capi.LORA_WINDOW_NONE, 1: _capi.LORA_WINDOW_HANN}
-_MODES = {"legacy": _capi.LORA_MODE_LEGACY, "api": _capi.LORA_MODE_API}
+_MODES = {"legacy": _capi.LORA_MODE_LEGACY, "api": _capi.LORA_MODE_API, "raw": _capi.LORA_MODE_RAW}
 
 
 @dataclass

@@ -542,6 +542,36 @@ void orc_demod_frames(const float* iq, size_t frames, size_t frame_len, unsigned
   for (auto& th : pool) th.join();
 }
 
+// LORA_MODE_RAW checker: the detector primitive alone per whole symbol
+// (LoRaDetector.hpp:39-58 on the (caller-dechirped, e2e_chain_test.cpp:88-93) and
+// windowed samples; no normalisation, estimate or rotation) - the demodulator of
+// tests/awgn_sweep.py:262-265 in fp32.  Returns the number of symbols.
+size_t orc_raw_demod(const float* iq, size_t count, unsigned sf, int hann, unsigned osr, int dechirp,
+                     float bw_scale, uint16_t* out_syms) {
+  static thread_local DemodState st;
+  if (st.sf != sf || st.hann != (hann != 0) || st.N == 0) demod_init(st, sf, hann != 0);
+  if (osr == 0) osr = 1;
+  const size_t N = st.N, step = N * osr, total = count / step;
+  std::vector<cf> down;
+  if (dechirp) {
+    down.resize(step);
+    float ph = 0.0f;
+    gen_chirp(down.data(), (int)N, (int)osr, (int)step, 0.0f, true, 1.0f, ph, bw_scale);
+  }
+  const cf* x = reinterpret_cast<const cf*>(iq);
+  for (size_t s = 0; s < total; ++s) {
+    for (size_t i = 0; i < N; ++i) {
+      const size_t j = s * step + i * osr;
+      cf v = x[j];
+      if (dechirp) v = cmul(v, down[j % step]);
+      st.fin[i] = cscale(v, st.window[i]);
+    }
+    float p, fi;
+    out_syms[s] = (uint16_t)detect(st.plan, st.fin, st.fout, st.power_scale, p, fi);
+  }
+  return total;
+}
+
 long orc_api_demodulate(const float* iq, size_t count, unsigned sf, int hann, unsigned osr,
                         float bw_scale, uint16_t* syms, size_t cap, uint8_t* out_sync,
                         float* out_cfo, float* out_toff) {

@@ -178,11 +178,22 @@ class Oracle(_Common):
                                            C.c_void_p, C.c_void_p]
         L.orc_compensate_offsets.argtypes = [_f32p, C.c_size_t, C.c_uint, C.c_uint, C.c_float,
                                              C.c_float]
+        L.orc_raw_demod.restype = C.c_size_t
+        L.orc_raw_demod.argtypes = [_f32p, C.c_size_t, C.c_uint, C.c_int, C.c_uint, C.c_int,
+                                    C.c_float, _u16p]
         L.orc_lora_encode.restype = C.c_size_t
         L.orc_lora_encode.argtypes = [_u8p, C.c_size_t, _u16p]
         L.orc_lora_decode.restype = C.c_size_t
         L.orc_lora_decode.argtypes = [_u16p, C.c_size_t, _u8p]
         L.orc_awgn_gtest_frames.restype = C.c_size_t
+
+    def raw_demod(self, iq, sf, osr=1, hann=False, dechirp=False, bw=125000):
+        """LORA_MODE_RAW checker: per-symbol (dechirp) -> window -> FFT -> argmax."""
+        x = _c64(iq)
+        out = np.zeros(max(len(x) // ((1 << sf) * osr), 1), np.uint16)
+        n = self.lib.orc_raw_demod(x.view(np.float32), len(x), sf, int(hann), osr, int(dechirp),
+                                   C.c_float(BW_SCALE[bw]), out)
+        return out[:n]
 
     def twiddles(self, N):
         out = np.empty(N, np.complex64)

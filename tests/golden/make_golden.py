@@ -239,6 +239,22 @@ def awgn_sweep_table() -> dict:
     mod = importlib.util.module_from_spec(spec)
     sys.modules["ref_awgn_sweep"] = mod  # the module's dataclass needs this
     spec.loader.exec_module(mod)
+    # Host-side pieces of the script, recorded so the CPU suite can pin our restatement
+    # (lora_phy_amd.awgn) without the script.
+    rng = np.random.default_rng(77)
+    pay = rng.integers(0, 256, 16).astype(np.uint8).tobytes()
+    pieces = {"payload": pay.hex(), "dec_h84": [list(map(int, mod.decode_hamming84(c))) for c in range(256)]}
+    for cr in ("4/5", "4/8"):
+        bits = mod.encode_payload(pay, cr)
+        pieces["bits_" + cr] = bits
+        for sf in (7, 9, 12):
+            syms = mod.bits_to_symbols(bits, sf)
+            pieces[f"syms_{cr}_sf{sf}"] = syms
+            back = mod.symbols_to_bits(syms, sf, len(bits))
+            assert back == bits
+        pieces["decoded_" + cr] = mod.decode_payload(bits, cr, len(pay))
+    up, down = mod.make_chirps(7)
+    pieces["up7_sha"] = hashlib.sha256(np.ascontiguousarray(up).tobytes()).hexdigest()
     rows = []
     for sf in (7, 8, 9):
         up, down = mod.make_chirps(sf)
@@ -247,7 +263,7 @@ def awgn_sweep_table() -> dict:
             for cr in ("4/5", "4/8"):
                 ber, per = mod.simulate(sf, cr, snr, 20, 16, up, down)
                 rows.append({"sf": sf, "cr": cr, "snr_db": snr, "ber": ber, "per": per})
-    return {"seed": 1234, "packets": 20, "payload_len": 16,
+    return {"seed": 1234, "packets": 20, "payload_len": 16, "pieces": pieces,
             "order": "per sf: seed(1234); for snr: for cr in (4/5, 4/8): simulate", "rows": rows}
 
 

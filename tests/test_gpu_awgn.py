@@ -1,0 +1,79 @@
+"""GPU: AWGN sweeps (BASELINE configs[3]).
+
+* ``awgn.simulate`` reproduces the reference script tests/awgn_sweep.py: same RNG draws,
+  channel and FEC, with the FFT + argmax on the GPU (LORA_MODE_RAW).  Its BER/PER must
+  equal the table recorded from the script itself (tests/golden/awgn_sweep.json, seed
+  1234, SF7-9, SNR -15..0 dB, CR 4/5 and 4/8).  Tolerance: exact; a decision can only
+  differ where two FFT bins tie to within fp32 rounding (the script computes in
+  float64), which this seeded table does not hit.
+* ``awgn.sweep_chain`` (library chain with the 2-sync-symbol estimate and CFO
+  correction) is bit-exact against the oracle on the same noisy frames, with and
+  without an injected CFO.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "awgn_sweep.json")
+
+
+@pytest.fixture(scope="module")
+def awgn():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from lora_phy_amd import awgn
+
+    return awgn
+
+
+def test_simulate_matches_reference_script_table(awgn):
+    table = json.load(open(GOLD))
+    rows = iter(table["rows"])
+    for sf in (7, 8, 9):
+        up, down = awgn.make_chirps(sf)
+        np.random.seed(table["seed"])
+        for snr in (-15.0, -10.0, -5.0, 0.0):
+            for cr in ("4/5", "4/8"):
+                want = next(rows)
+                assert (want["sf"], want["snr_db"], want["cr"]) == (sf, snr, cr)
+                ber, per = awgn.simulate(sf, cr, snr, table["packets"], table["payload_len"], up, down)
+                assert ber == pytest.approx(want["ber"], abs=0.0), (sf, snr, cr)
+                assert per == pytest.approx(want["per"], abs=0.0), (sf, snr, cr)
+
+
+def test_simulate_raw_decisions_equal_oracle(awgn):
+    from oracle.pyoracle import Oracle
+
+    O = Oracle()
+    up, down = awgn.make_chirps(8)
+    np.random.seed(7)
+    _, _, rx, rows = awgn.simulate(8, "4/8", -9.0, 6, 16, up, down, return_symbols=True)
+    x = rows.astype(np.complex64)
+    want = np.array([O.raw_demod(r, 8)[0] for r in x])
+    np.testing.assert_array_equal(rx, want)
+
+
+@pytest.mark.parametrize("sf,cfo", [(7, 0.0), (7, 0.37), (9, 0.0), (10, -0.8), (12, 0.2)])
+def test_chain_sweep_bit_exact_vs_oracle(awgn, sf, cfo):
+    from oracle.pyoracle import Oracle
+
+    O = Oracle()
+    frames = 24 if sf < 12 else 6
+    recs = awgn.sweep_chain(sf, [-12.0, -6.0, 0.0, 10.0], frames=frames, payload_len=8, seed=sf,
+                            cfo_bins=cfo, keep_iq=True)
+    for r in recs:
+        x = r["iq"].cpu().numpy()
+        syms, sync, cfo_o, toff, _ = O.demod_frames(x, sf, 1, False, dechirp=True, threads=8)
+        got = r["result"]
+        S = got.symbols.shape[1]
+        np.testing.assert_array_equal(got.symbols.cpu().numpy(), syms[:, :S])
+        np.testing.assert_array_equal(got.sync.cpu().numpy(), sync)
+        np.testing.assert_array_equal(got.cfo.cpu().numpy().view(np.uint32), cfo_o.view(np.uint32))
+        np.testing.assert_array_equal(got.time_offset.cpu().numpy().view(np.uint32), toff.view(np.uint32))
+    if cfo == 0.0:
+        assert recs[-1]["per"] == 0.0  # +10 dB, no CFO: every packet decodes

@@ -226,3 +226,33 @@ def test_pipelined_batch_matches_oracle(O, amd, sf, F, nsym, hann, dechirp, mode
     np.testing.assert_array_equal(res.sync.cpu().numpy(), osync)
     np.testing.assert_array_equal(bits(res.cfo.cpu().numpy()), bits(ocfo))
     np.testing.assert_array_equal(bits(res.time_offset.cpu().numpy()), bits(otoff))
+
+
+@pytest.mark.parametrize("path", ["fast", "generic"])
+@pytest.mark.parametrize("sf,osr,hann,dechirp", [(7, 1, False, True), (7, 1, False, False), (9, 2, True, True),
+                                                 (12, 1, False, True), (5, 3, True, False), (2, 1, False, False),
+                                                 (11, 1, True, True)])
+def test_raw_mode_matches_oracle(O, amd, sf, osr, hann, dechirp, path):
+    """LORA_MODE_RAW (detector only) vs the oracle's orc_raw_demod, any SNR."""
+    rng = np.random.default_rng(sf * 100 + osr)
+    N = 1 << sf
+    F, S = 6, 9
+    L = S * N * osr + 5
+    rows = []
+    for f in range(F):
+        syms = rng.integers(0, N, S - 2).astype(np.uint16)
+        x = O.lora_modulate(syms, sf, osr, 125000, 1.0, 0x12)
+        if not dechirp:
+            x = O.dechirp(x, sf, osr)
+        x = np.concatenate([x, np.zeros(5, np.complex64)])
+        sig = [0.0, 0.5, 2.0][f % 3]
+        x = (x + sig * (rng.standard_normal(L) + 1j * rng.standard_normal(L))).astype(np.complex64)
+        rows.append(x)
+    iq = np.stack(rows)
+    plan = make_plan(amd, path, sf, osr, 125000, "hann" if hann else "none", dechirp=dechirp, mode="raw")
+    res = plan.run(torch.from_numpy(iq).cuda())
+    got = res.symbols.cpu().numpy()
+    assert got.shape == (F, L // (N * osr))  # every whole symbol, sync symbols included
+    for f in range(F):
+        np.testing.assert_array_equal(got[f], O.raw_demod(iq[f], sf, osr, hann, dechirp=dechirp))
+    assert int(res.sync.to(torch.int32).sum()) == 0 and float(res.cfo.abs().sum()) == 0.0
