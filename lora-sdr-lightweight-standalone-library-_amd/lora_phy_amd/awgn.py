@@ -154,7 +154,9 @@ def sweep_chain(sf: int, snr_dbs: Sequence[float], frames: int = 1000, payload_l
         res = plan.run(iq)
         rx = res.symbols.to(torch.int64).cpu().numpy()
         dec = codes.lora_decode(rx)
-        ser = float((rx != tx).mean())
+        # the modulator sends each 8-bit Hamming codeword modulo N (SF7 drops bit 7,
+        # which the decoder then corrects), so symbol errors count against tx mod N
+        ser = float((rx != (tx % N)).mean())
         diff = np.bitwise_xor(dec, payloads)
         rec = {"sf": sf, "snr_db": float(snr), "frames": frames, "ser": ser,
                "ber": float(np.unpackbits(diff).mean()), "per": float(diff.any(1).mean()),
