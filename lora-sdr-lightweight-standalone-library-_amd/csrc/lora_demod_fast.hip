@@ -58,11 +58,62 @@ constexpr int leaf_pos(int R, int v) {
   return pos;
 }
 
-// Padded LDS address of DIT position p: one spare complex per R1 block breaks the
-// power-of-two stride of the pass-1 write-back (conflict-free ds_write_b64).
-template <int LOGR1>
-__device__ __forceinline__ int paddr(int p) {
-  return p + (p >> LOGR1);
+// LDS image of DIT position p: slot(p) = p + sum_{i>=0} bit_{4+i}(p) * W[i].  The
+// weights (and the row pad) were searched with tools/lds/lds_search_add.py against the
+// MI355X banking rules (ds_read_b64: 2 x 32 lanes, 64 banks; ds_write_b64: 4 x 16
+// lanes, 32 banks) over every access of the transform - pass-1 write-back, LDS-pass
+// reads and write-backs, natural-order write: mean conflict degree 1.0-1.4 (the
+// former p + p/R1 map reached 2-5.5, 16-way on the SF11/12 pass-1 write-back).  The
+// search keeps every weight >= the sum of the lower ones (injective, asserted below).
+// Being linear in the bits of p, slot(base | off) = slot(base) + slot(off) when base and
+// off use disjoint bits: every access splits into a per-lane part and a compile-time
+// part that folds into the ds_* immediate offset.
+template <int SF>
+struct LdsMap;
+template <> struct LdsMap<6> { static constexpr int W[2] = {1, 2}; static constexpr int PAD = 1; };
+template <> struct LdsMap<7> { static constexpr int W[3] = {1, 3, 4}; static constexpr int PAD = 0; };
+template <> struct LdsMap<8> { static constexpr int W[4] = {1, 2, 4, 8}; static constexpr int PAD = 1; };
+template <> struct LdsMap<9> { static constexpr int W[5] = {0, 1, 4, 8, 14}; static constexpr int PAD = 0; };
+template <> struct LdsMap<10> { static constexpr int W[6] = {0, 0, 1, 2, 4, 8}; static constexpr int PAD = 0; };
+template <> struct LdsMap<11> { static constexpr int W[7] = {0, 0, 2, 8, 10, 20, 43}; static constexpr int PAD = 0; };
+template <> struct LdsMap<12> { static constexpr int W[8] = {0, 0, 0, 0, 1, 2, 4, 8}; static constexpr int PAD = 0; };
+
+// Injectivity: each weight is at least the sum of the lower ones, so the offset of a
+// 16-position block is monotone in the block index and blocks never overlap.
+template <int SF>
+constexpr bool lds_map_injective() {
+  int acc = 0;
+  for (int i = 0; i < SF - 4; ++i) {
+    if (LdsMap<SF>::W[i] < acc) return false;
+    acc += LdsMap<SF>::W[i];
+  }
+  return true;
+}
+static_assert(lds_map_injective<6>() && lds_map_injective<7>() && lds_map_injective<8>() &&
+                  lds_map_injective<9>() && lds_map_injective<10>() && lds_map_injective<11>() &&
+                  lds_map_injective<12>(),
+              "LDS slot map must be injective");
+
+template <int SF>
+__host__ __device__ constexpr int lds_slot(int p) {
+  if constexpr (SF <= 5) {
+    return p;
+  } else {
+    int s = p;
+    for (int i = 0; i < SF - 4; ++i) s += ((p >> (4 + i)) & 1) * LdsMap<SF>::W[i];
+    return s;
+  }
+}
+
+template <int SF>
+constexpr int lds_row() {  // complex elements per symbol row
+  if constexpr (SF <= 5) {
+    return 1 << SF;
+  } else {
+    int w = 0;
+    for (int i = 0; i < SF - 4; ++i) w += LdsMap<SF>::W[i];
+    return (1 << SF) + w + LdsMap<SF>::PAD;
+  }
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -108,7 +159,7 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ t
 
 // The other lanes' share of one pass: read R points from LDS, run the stages,
 // either write them back or fold them into the argmax key.
-template <int R, int N, int MA, int LOGR1, int T, int P, bool LAST>
+template <int R, int N, int MA, int SF, int T, int P, bool LAST>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
                                          uint64_t& key) {
   constexpr int NG = P / R;
@@ -117,8 +168,9 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     const int GI = l + T * gg;
     const int k = GI % MA, cc = GI / MA;
     cf* xs = x + gg * R;
+    const cf* rb = row + lds_slot<SF>(cc * MA * R + k);  // k < MA, MA*u: disjoint bits
 #pragma unroll
-    for (int u = 0; u < R; ++u) xs[u] = row[paddr<LOGR1>(cc * MA * R + k + MA * u)];
+    for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
     pass_regs<R, false, N, MA>(xs, k, tw);
   }
   if constexpr (LAST) {
@@ -143,15 +195,16 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
   }
 }
 
-template <int R, int MA, int LOGR1, int T, int P>
+template <int R, int MA, int SF, int T, int P>
 __device__ __forceinline__ void write_pass(cf* row, const cf* x, int l) {
   constexpr int NG = P / R;
 #pragma unroll
   for (int gg = 0; gg < NG; ++gg) {
     const int GI = l + T * gg;
     const int k = GI % MA, cc = GI / MA;
+    cf* rb = row + lds_slot<SF>(cc * MA * R + k);
 #pragma unroll
-    for (int u = 0; u < R; ++u) row[paddr<LOGR1>(cc * MA * R + k + MA * u)] = x[gg * R + u];
+    for (int u = 0; u < R; ++u) rb[lds_slot<SF>(MA * u)] = x[gg * R + u];
   }
 }
 
@@ -292,18 +345,18 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
 #pragma unroll
     for (int h = 0; h < G::G1; ++h)
 #pragma unroll
-      for (int u = 0; u < R1; ++u) row[paddr<G::LOGR1>(c[h] * R1 + u)] = z[h * R1 + u];
+      for (int u = 0; u < R1; ++u) row[lds_slot<SF>(c[h] * R1) + u] = z[h * R1 + u];  // u < 16
     block_sync<WL>();
     constexpr int RL = G::NPASS == 2 ? G::RA : G::RB;   // last pass span
     constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, G::LOGR1, T, P, true>(row, z, l, a.tw, key);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row, z, l, a.tw, key);
     } else {
-      pass_lds<G::RA, N, G::MA_A, G::LOGR1, T, P, false>(row, z, l, a.tw, key);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, false>(row, z, l, a.tw, key);
       block_sync<WL>();
-      write_pass<G::RA, G::MA_A, G::LOGR1, T, P>(row, z, l);
+      write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
       block_sync<WL>();
-      pass_lds<G::RB, N, G::MA_B, G::LOGR1, T, P, true>(row, z, l, a.tw, key);
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true>(row, z, l, a.tw, key);
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)
@@ -311,7 +364,7 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
 #pragma unroll
       for (int gg = 0; gg < P / RL; ++gg)
 #pragma unroll
-        for (int u = 0; u < RL; ++u) row[paddr<G::LOGR1>(l + T * gg + ML * u)] = z[gg * RL + u];
+        for (int u = 0; u < RL; ++u) row[lds_slot<SF>(l + T * gg) + lds_slot<SF>(ML * u)] = z[gg * RL + u];
       block_sync<WL>();
     }
   }
@@ -447,9 +500,9 @@ __global__ void __launch_bounds__(256) k_est_fast(KArgs a, int64_t frames, int r
             if ((uint32_t)u == idx) B = z[u];
           }
         } else {
-          L = row[paddr<G::LOGR1>((int)im1)];
-          R = row[paddr<G::LOGR1>((int)ip1)];
-          B = row[paddr<G::LOGR1>((int)idx)];
+          L = row[lds_slot<SF>((int)im1)];
+          R = row[lds_slot<SF>((int)ip1)];
+          B = row[lds_slot<SF>((int)idx)];
         }
         float pw, fi;
         detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
@@ -525,12 +578,7 @@ __global__ void __launch_bounds__(256) k_est_fast(KArgs a, int64_t frames, int r
 
 template <int SF>
 int row_complex() {
-  using G = Geo<SF>;
-  int rowc = G::N + (G::N >> G::LOGR1);  // padded transpose image
-  // rows 16-byte aligned and staggered by 16 banks (rowc = 8 mod 32 complex) so the
-  // symbols of one wave hit different banks in the strided pass-1 gather
-  while (rowc % 32 != 8) ++rowc;
-  return rowc;
+  return lds_row<SF>();
 }
 
 template <int SF, int MODE>
