@@ -446,8 +446,11 @@ __global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t wor
 // fractional index, LoRaDetector.hpp:60-71) and the phase of that bin; lane 0 keeps
 // the estimator state.  Then symbols 0/1 are demodulated with the estimated offsets
 // exactly as k_demod_fast does for the data symbols, giving the sync word.
+// Latency-bound (a few sequential transforms per frame): occupancy matters more than
+// ILP, so the register budget is capped at two waves per SIMD.
 template <int SF, int MODE>
-__global__ void __launch_bounds__(256) k_est_fast(KArgs a, int64_t frames, int rowc) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+k_est_fast(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
   constexpr int SPB = (T >= 64 ? 256 : 64) / T;  // frames per block (block = max(T, 64))
