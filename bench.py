@@ -54,10 +54,13 @@ def dist_setup(n_gpus):
     return None, 0, 1
 
 
+SYNC = 0x12
+
+
 def make_input(sf, frames, data_syms, seed, device, snr_db=None):
     g = torch.Generator(device="cpu").manual_seed(seed)
     syms = torch.randint(0, 1 << sf, (frames, data_syms), generator=g, dtype=torch.int32)
-    iq = amd.modulate(syms.to(device), sf, 1, 125000, 1.0, 0x12)
+    iq = amd.modulate(syms.to(device), sf, 1, 125000, 1.0, SYNC)
     if snr_db is not None:
         sigma = 10.0 ** (-snr_db / 20.0) / np.sqrt(2.0)
         gn = torch.Generator(device=device).manual_seed(seed + 1)
@@ -194,7 +197,12 @@ def main():
     ap.add_argument("--sf12-only", action="store_true", help="profiling: SF12 workload only")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--sync", type=lambda v: int(v, 0), default=0x12,
+                    help="sync word of the synthetic frames (0x12 = the reference default; "
+                         "large nibbles -> large estimated CFO -> phases past the fast sincos range)")
     args = ap.parse_args()
+    global SYNC
+    SYNC = args.sync
 
     dist, rank, world = dist_setup(args.gpus)
     device = torch.device("cuda", torch.cuda.current_device())

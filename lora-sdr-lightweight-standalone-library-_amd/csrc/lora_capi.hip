@@ -510,22 +510,43 @@ __global__ void k_mod_phase(ModArgs a) {
   }
 }
 
-__global__ void k_mod_samples(ModArgs a) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= a.frames * a.nchirp) return;
-  const int64_t fr = w / a.nchirp;
-  const int c = (int)(w - fr * a.nchirp);
-  cf* out = a.iq + w * a.step;
-  float phase = out[0].re;
+// One 64-lane workgroup per 64 chirps.  The genChirp recurrence (ChirpGenerator.hpp:
+// 118-128: f += fStep, wrap, phase += f, all fp32) is inherently sequential, so each
+// lane advances its own chirp 64 samples at a time into an LDS tile; the wave then
+// evaluates sincosf over the transposed tile, so that for every chirp 64 consecutive
+// samples (512 B) are stored by one coalesced instruction.
+constexpr int kModLanes = 64;
+__global__ void __launch_bounds__(kModLanes) k_mod_samples(ModArgs a) {
+  __shared__ float tile[kModLanes][kModLanes + 1];  // [chirp][sample], padded row
+  const int lane = threadIdx.x;
+  const int64_t nch = a.frames * (int64_t)a.nchirp;
+  const int64_t w0 = (int64_t)blockIdx.x * kModLanes;
+  const int64_t w = w0 + lane;
+  const bool valid = w < nch;
+  const int64_t wc = valid ? w : nch - 1;
+  const int64_t fr = wc / a.nchirp;
+  const int c = (int)(wc - fr * a.nchirp);
+  float phase = a.iq[wc * a.step].re;  // start phase from k_mod_phase
   float f = a.fMin + chirp_f0(a, fr, c);
   const float span = a.fMax - a.fMin;
-  for (int i = 0; i < a.step; ++i) {
-    f += a.fStep;
-    if (f > a.fMax) f -= span;
-    phase += f;
-    float s, co;
-    lm_sincosf(phase, &s, &co);
-    out[i] = cf{a.ampl * co, a.ampl * s};
+  const int nvalid = (int)min((int64_t)kModLanes, nch - w0);
+  for (int i0 = 0; i0 < a.step; i0 += kModLanes) {
+    const int cnt = min(kModLanes, a.step - i0);
+    for (int j = 0; j < cnt; ++j) {
+      f += a.fStep;
+      if (f > a.fMax) f -= span;
+      phase += f;
+      tile[lane][j] = phase;
+    }
+    __syncthreads();  // single wave: orders the tile writes before the reads
+    if (lane < cnt) {
+      for (int ch = 0; ch < nvalid; ++ch) {
+        float sn, cs;
+        lm_sincosf_bf(tile[ch][lane], &sn, &cs);
+        a.iq[(w0 + ch) * a.step + i0 + lane] = cf{a.ampl * cs, a.ampl * sn};
+      }
+    }
+    __syncthreads();
   }
 }
 

@@ -300,12 +300,12 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
         z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
       }
     }
-  } else {
+  } else {  // some phase beyond the fast range: branch-free reduction select per point
 #pragma unroll
     for (int q = 0; q < P; ++q) {
       const float ph = start + rate * (float)(l + T * q);
       float sn, cs;
-      lm_sincosf(ph, &sn, &cs);
+      lm_sincosf_bf(ph, &sn, &cs);
       cf v = cmul(in[q], cf{cs, sn});
       if (hann) v = cscale(v, win[l + T * q]);
       z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;

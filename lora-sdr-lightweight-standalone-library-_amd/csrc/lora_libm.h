@@ -283,6 +283,48 @@ LM_FN void lm_sincosf_fast_k_nz(const float* y, float* sinp, float* cosp) {
   }
 }
 
+// Branch-free lm_sincosf for every input (same results, including -0, inf and NaN):
+// both of glibc's argument reductions are evaluated - reduce_fast (|y| < 120, which
+// also reproduces the |y| < pi/4 and tiny paths, see lm_sincosf_fast) and the
+// Payne-Hanek reduce_large - and selected per element, then one polynomial.  For a
+// wave whose phases straddle 120 or lie beyond it (large CFO, long frames, the
+// modulator's in-chirp phase) this replaces lm_sincosf's divergent branches.
+LM_FN void lm_sincosf_bf(float y, float* sinp, float* cosp) {
+  const uint32_t top = lm_abstop12(y);
+  const double x = (double)y;
+  // reduce_fast
+  const int nf = (((int32_t)(x * LM_SC_HPI_INV)) + 0x800000) >> 24;
+  const double xf = lm_fma(-(double)nf, LM_SC_HPI, x);
+  // reduce_large (valid for finite |y| >= 120; computed regardless, selected below)
+  uint32_t xi = lm_asuint(y);
+  const int sign = (int)(xi >> 31);
+  const uint32_t* arr = &LM_INV_PIO4[(xi >> 26) & 15];
+  const int shift = (xi >> 23) & 7;
+  xi = (xi & 0xffffffu) | 0x800000u;
+  xi <<= shift;
+  uint64_t res0 = (uint64_t)(uint32_t)(xi * arr[0]);
+  const uint64_t res1 = (uint64_t)xi * arr[4];
+  const uint64_t res2 = (uint64_t)xi * arr[8];
+  res0 = (res2 >> 32) | (res0 << 32);
+  res0 += res1;
+  const uint64_t nn = (res0 + (1ull << 61)) >> 62;
+  res0 -= nn << 62;
+  const double xl = (double)(int64_t)res0 * LM_PI63;
+  const bool large = top >= 0x42fu;
+  const double xr = large ? xl : xf;
+  const int n = large ? (int)nn : nf;
+  const int nq = large ? (int)nn + sign : nf;
+  const double xs = ((nq ^ (nq >> 1)) & 1) ? -xr : xr;
+  float sv, cv;
+  lm_sincosf_poly(xs, xr * xr, (nq & 2) != 0, &sv, &cv);
+  float so = (n & 1) ? cv : sv;
+  float co = (n & 1) ? sv : cv;
+  if (y == 0.0f) so = y;  // sin(-0) = -0 (glibc's tiny path)
+  if (top >= 0x7f8u) so = co = y - y;  // inf / NaN
+  *sinp = so;
+  *cosp = co;
+}
+
 // True when lm_sincosf_fast is exact for y.
 LM_FN int lm_sincosf_fast_ok(float y) { return lm_abstop12(y) < 0x42fu; }
 
