@@ -42,13 +42,22 @@ def log(*a):
 
 
 def dist_setup(n_gpus):
+    """One process per GPU (torchrun).  The collectives are only the timing barrier and
+    the max/sum all-reduces (lora_phy_amd.shard); frames never cross GPUs.  Backend
+    "nccl" (RCCL) by default; LORA_BENCH_BACKEND=gloo rehearses the multi-rank path with
+    several ranks on fewer GPUs (ranks share devices round-robin)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         import torch.distributed as dist
 
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("LORA_BENCH_BACKEND", "nccl")
+        dev = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
         return dist, dist.get_rank(), world
     torch.cuda.set_device(0)
     return None, 0, 1
