@@ -66,6 +66,18 @@ def main():
     for (k, wg), a in sorted(agg.items(), key=lambda kv: -kv[1]["ns"]):
         lines.append(f"| `{k}` | {wg} | {a['calls']} | {a['ns'] / a['calls'] / 1e3:.2f} | "
                      f"{a['ns'] / 1e3:.1f} | {a['lds']} | {a['vgpr']} | {a['sgpr']} | {a['scratch']} |")
+    # the bench's own HIP-event kernel times from the SAME profiled run, for comparison
+    try:
+        runs = [json.loads(l) for l in open(os.path.join(src, "kt.log")) if l.startswith("{")]
+        for r in runs:
+            st = r["config"]["stage_ms"]
+            lines += ["", "bench.py HIP-event averages in the same profiled run (ms): SF7 frame max "
+                      f"{st[0]:.4f}, estimate {st[1]:.4f}, demod {st[2]:.4f}"]
+            if "sf12" in r.get("extra", {}):
+                s12 = r["extra"]["sf12"]["stage_ms"]
+                lines += [f"SF12 frame max {s12[0]:.3f}, estimate {s12[1]:.3f}, demod {s12[2]:.3f}"]
+    except (OSError, ValueError, KeyError):
+        pass
     open(os.path.join(dst, "kernel_stats.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
