@@ -134,6 +134,51 @@ def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=
     }
 
 
+def run_channels(frames, data_syms, steps, warmup, rank, dist, device, chunk_bytes=8e9):
+    """BASELINE.json configs[4]: one channel per GPU, `frames` SF7 frames of 2 + `data_syms`
+    symbols resident in HBM (18.4 GB at 1e6 x 16), demodulated in <= 8 GB chunks per step
+    (SURVEY.md 8d item 5).  Inputs generated on the device (GPU modulator) in slices."""
+    sf, N = 7, 128
+    L = (data_syms + 2) * N
+    iq = torch.empty((frames, L), dtype=torch.complex64, device=device)
+    g = torch.Generator(device="cpu").manual_seed(4242 + rank)
+    gen_rows = 1 << 17
+    first_syms = None
+    for r0 in range(0, frames, gen_rows):
+        n = min(gen_rows, frames - r0)
+        syms = torch.randint(0, N, (n, data_syms), generator=g, dtype=torch.int32)
+        if first_syms is None:
+            first_syms = syms[:64].clone()
+        iq[r0:r0 + n] = amd.modulate(syms.to(device), sf, 1, 125000, 1.0, SYNC)
+    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device)
+    per_chunk = max(1, int(chunk_bytes // (L * 8)))
+    chunks = [(c0, min(per_chunk, frames - c0)) for c0 in range(0, frames, per_chunk)]
+    outs = [None] * len(chunks)
+
+    def step():
+        for i, (c0, n) in enumerate(chunks):
+            outs[i] = plan.run(iq[c0:c0 + n], outs[i])
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(device)
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    units, wall_max, _ = aggregate_throughput(frames * data_syms * steps, wall)
+    ok = bool(torch.equal(outs[0].symbols[:64].to(torch.int32).cpu(), first_syms))
+    del iq
+    return {"frames_per_gpu": frames, "data_symbols_per_frame": data_syms, "iq_gb_per_gpu": frames * L * 8 / 1e9,
+            "chunks": len(chunks), "ms_per_step": wall_max * 1e3 / steps,
+            "value_all_ranks_msym_s": units / wall_max / 1e6, "symbols_ok_first64": ok}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -205,6 +250,8 @@ def main():
     ap.add_argument("--no-sf12", action="store_true")
     ap.add_argument("--sf12-only", action="store_true", help="profiling: SF12 workload only")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-channels", action="store_true", help="skip the configs[4] measurement")
+    ap.add_argument("--channel-frames", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--sync", type=lambda v: int(v, 0), default=0x12,
                     help="sync word of the synthetic frames (0x12 = the reference default; "
@@ -230,6 +277,10 @@ def main():
         extra["sf12"]["value_all_ranks_msym_s"] = r12["msym_s_all_ranks"]
         extra["sf12"]["roofline_frac"] = r12["dominant_gbs"] / HBM_PEAK_GBS
         del r12
+        torch.cuda.empty_cache()
+    if not args.no_channels and not args.sf12_only:
+        extra["channels"] = run_channels(args.channel_frames, 16, max(args.steps // 4, 2), 1, rank, dist,
+                                         device)
         torch.cuda.empty_cache()
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:

@@ -66,6 +66,26 @@ def chain(R: Reference, sf: int, bw: int, syms: np.ndarray, bw_scale: float) -> 
     return rec
 
 
+def capture(R: Reference) -> dict:
+    """Real capture shipped with the reference (vectors_binary/bw_125k_sf_7_cr_1_ldro_
+    false_crc_true_implheader_false.unknown, 267,264 complex64 samples):
+    the first 32,768 samples are kept as a data fixture and run through the reference's
+    lora_demodulate as one frame, raw and caller-dechirped, osr 1/2/4, both windows."""
+    src = os.path.join(REF_ROOT, "vectors_binary",
+                       "bw_125k_sf_7_cr_1_ldro_false_crc_true_implheader_false.unknown")
+    x = np.fromfile(src, dtype=np.complex64)[:32768]
+    x.tofile(os.path.join(HERE, "capture_sf7_excerpt.iq"))
+    cases = []
+    for osr in (1, 2, 4):
+        for dech in (False, True):
+            for hann in (False, True):
+                xi = dechirp(R, x, 7, osr) if dech else x
+                rec = demod_record(R, xi, 7, osr, hann)
+                rec.update({"osr": osr, "dechirp": dech, "hann": hann})
+                cases.append(rec)
+    return {"file": "capture_sf7_excerpt.iq", "sha256": sha(x), "sf": 7, "cases": cases}
+
+
 def e2e(R: Reference) -> list:
     """tests/e2e_chain_test.cpp:62-113: 32-byte ramp payload, profiles.yaml profiles."""
     out = []
@@ -282,6 +302,7 @@ def main() -> None:
         "stress": stress(R),
         "api": api_cases(R),
         "codes": codes(R),
+        "capture": capture(R),
     }
     with open(os.path.join(HERE, "golden.json"), "w") as fh:
         json.dump(gold, fh, indent=1)

@@ -128,3 +128,13 @@ def test_api_cases(G, O):
         assert f32bits(ocfo) == rec["cfo_bits"] and f32bits(otoff) == rec["toff_bits"]
         ecfo, etoff = O.estimate_offsets(x, sf, osr, hann)
         assert f32bits(ecfo) == rec["est_cfo_bits"] and f32bits(etoff) == rec["est_toff_bits"]
+
+
+def test_capture_excerpt(G, O):
+    """The reference's real SF7 capture (excerpt), every osr / dechirp / window case."""
+    cap = G["capture"]
+    x = np.fromfile(os.path.join(GOLD, cap["file"]), dtype=np.complex64)
+    assert sha(x) == cap["sha256"]
+    for rec in cap["cases"]:
+        xi = dechirp(O, x, 7, rec["osr"]) if rec["dechirp"] else x
+        check(rec, O.lora_demodulate(xi, 7, rec["osr"], rec["hann"]))

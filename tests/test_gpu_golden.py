@@ -137,3 +137,16 @@ def test_api_cases_gpu(G, O, amd):
         plan.estimate_offsets(torch.from_numpy(x).cuda(), cfo, toff)
         assert f32bits(cfo.item()) == rec["est_cfo_bits"]
         assert f32bits(toff.item()) == rec["est_toff_bits"]
+
+
+def test_capture_excerpt_gpu(G, amd):
+    """Real capture from the reference (vectors_binary, SF7): one long frame, GPU vs the
+    reference's lora_demodulate for osr 1/2/4, raw and fused dechirp, both windows."""
+    cap = G["capture"]
+    x = np.fromfile(os.path.join(GOLD, cap["file"]), dtype=np.complex64)
+    assert sha(x) == cap["sha256"]
+    xt = torch.from_numpy(x).cuda()
+    for rec in cap["cases"]:
+        plan = amd.DemodPlan(7, rec["osr"], 125000, "hann" if rec["hann"] else "none",
+                             dechirp=rec["dechirp"])
+        check_frame(plan.run(xt), 0, rec)
