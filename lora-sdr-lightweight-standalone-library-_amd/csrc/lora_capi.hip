@@ -114,11 +114,10 @@ float bw_scale_of(unsigned bw_hz) { return static_cast<float>(bw_hz) / 125000.0f
 
 bool bw_ok(unsigned bw) { return bw == 125000 || bw == 250000 || bw == 500000; }
 
-// Workspace: per-frame max bits and arrival counters (zeroed per batch, 16-byte
-// multiple), then per-frame FrameParams.
-int64_t ws_slots(int64_t frames) { return (frames + 3) & ~int64_t(3); }
-size_t ws_counter_bytes(int64_t frames) {
-  return ((size_t)ws_slots(frames) * 2 * sizeof(uint32_t) + 255) & ~size_t(255);
+// Workspace: per-frame partial maxima (written by k_frame_max, no zeroing pass), then
+// per-frame FrameParams.
+size_t ws_counter_bytes(int64_t frames) {  // partial maxima, kMaxBpf per frame
+  return ((size_t)frames * lora::kMaxBpf * sizeof(uint32_t) + 255) & ~size_t(255);
 }
 
 // ---------------------------------------------------------------------------------
@@ -309,15 +308,15 @@ __device__ __forceinline__ void estimate_frame(const KArgs& a, int f, int scaled
 __global__ void __launch_bounds__(256) k_estimate(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float maxv = 0.0f;
-  if (a.mode == LORA_MODE_LEGACY && !a.est_only) maxv = __uint_as_float(a.maxbits[blockIdx.x]);
+  if (a.mode == LORA_MODE_LEGACY && !a.est_only) maxv = lora::frame_maxv(a, blockIdx.x);
   const int scaled = maxv > 1.0f;
   estimate_frame(a, blockIdx.x, scaled, scaled ? 1.0f / maxv : 1.0f, maxv,
                  reinterpret_cast<cf*>(smem));
 }
 
 // LEGACY: per-frame max(|I|,|Q|) of the (dechirped) samples (LoRaDemod.cpp:59-67),
-// streamed by `bpf` blocks per frame (`chunk` samples each, 16-byte loads) and reduced
-// with one atomicMax per block into maxbits (zeroed before the launch).
+// streamed by `bpf` blocks per frame (`chunk` samples each, 16-byte loads); block c
+// stores its partial maximum in maxbits[f*bpf + c] (the estimate reduces them).
 __global__ void __launch_bounds__(256) k_frame_max(KArgs a, int bpf, int chunk,
                                                    uint32_t* __restrict__ maxbits) {
   __shared__ float wmax[4];
@@ -384,7 +383,7 @@ __global__ void __launch_bounds__(256) k_frame_max(KArgs a, int bpf, int chunk,
   __syncthreads();
   if (threadIdx.x == 0) {
     const float r = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
-    if (r > 0.0f) atomicMax(&maxbits[f], __float_as_uint(r));
+    maxbits[f * a.mx_bpf + c] = __float_as_uint(r);  // partial c of frame f
   }
 }
 
@@ -838,8 +837,16 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
 
   const int s0 = a.have_sync ? 2 : 0;
   const int64_t per = total - s0;
-  const int bpf = frame_len > 0 ? (int)((frame_len + 4095) / 4096) : 1;
-  // <= 8 pairs per thread per block (one batch of k_frame_max), split evenly
+  // samples per k_frame_max block (experiment knob LORA_MI355X_MAXCHUNK, default 4096)
+  static const int max_chunk = [] {
+    const char* e = std::getenv("LORA_MI355X_MAXCHUNK");
+    const int v = e ? std::atoi(e) : 4096;
+    return v >= 512 ? v : 4096;
+  }();
+  const int bpf = frame_len > 0 ? (int)std::min<int64_t>(lora::kMaxBpf, (frame_len + max_chunk - 1) / max_chunk)
+                                : 1;
+  a.mx_bpf = (p.mode == LORA_MODE_LEGACY && frame_len > 0) ? bpf : 0;
+  // split evenly over the frame's blocks
   const int chunk = (int)((((frame_len + bpf - 1) / bpf) + 1) & ~int64_t(1));
   if (frames * bpf >= (int64_t(1) << 31)) {
     if (prev != p.device) hipSetDevice(prev);
@@ -868,7 +875,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   auto chunk_args = [&](int64_t c0) {
     KArgs ac = a;
     ac.iq = a.iq + c0 * frame_stride;
-    ac.maxbits = a.maxbits + c0;
+    ac.maxbits = a.maxbits + c0 * bpf;
     ac.fp = a.fp + c0;
     if (ac.syms) ac.syms = a.syms + c0 * a.sym_stride;
     if (ac.sync) ac.sync = a.sync + c0;
@@ -889,8 +896,6 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     if (e != hipSuccess) rc = set_error(LORA_EIO, "hipMemsetAsync failed");
     if (rc == LORA_OK) demod(a, frames, st);
   } else if (nchunks <= 1) {
-    if (p.mode == LORA_MODE_LEGACY && hipMemsetAsync(maxbits, 0, ws_counter_bytes(frames), st) != hipSuccess)
-      rc = set_error(LORA_EIO, "hipMemsetAsync failed");
     if (rc == LORA_OK) {
       prep(a, maxbits, frames, st);
       demod(a, frames, st);
@@ -901,12 +906,10 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     hipStream_t ax = plan->aux;
     hipEventRecord(plan->ev_fork, st);
     hipStreamWaitEvent(ax, plan->ev_fork, 0);
-    if (p.mode == LORA_MODE_LEGACY && hipMemsetAsync(maxbits, 0, ws_counter_bytes(frames), ax) != hipSuccess)
-      rc = set_error(LORA_EIO, "hipMemsetAsync failed");
     const int64_t fpc = (frames + nchunks - 1) / nchunks;
     for (int c = 0; c < nchunks && rc == LORA_OK; ++c) {
       const int64_t c0 = c * fpc, nf = std::min(fpc, frames - c0);
-      if (nf > 0) prep(chunk_args(c0), maxbits + c0, nf, ax);
+      if (nf > 0) prep(chunk_args(c0), maxbits + c0 * bpf, nf, ax);
       hipEventRecord(plan->ev_chunk[c], ax);
     }
     for (int c = 0; c < nchunks && rc == LORA_OK; ++c) {
@@ -1001,6 +1004,7 @@ int64_t lora_estimate_offsets_batch(lora_demod_plan* plan, const float* iq, int6
   a.down1 = plan->down1;
   a.cfo = cfo;
   a.toff = time_offset;
+  a.mx_bpf = 0;
   a.est_only = 1;
   hipLaunchKernelGGL(k_estimate, dim3((unsigned)frames), dim3(256), sizeof(cf) * plan->N,
                      static_cast<hipStream_t>(stream), a);

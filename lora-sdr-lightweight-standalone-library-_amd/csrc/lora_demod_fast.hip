@@ -471,7 +471,7 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
   const int64_t f = valid ? f0 : frames - 1;
   const cf* __restrict__ x = a.iq + f * a.frame_stride;
   cf* row = reinterpret_cast<cf*>(smem) + (size_t)g * rowc;
-  const float maxv = legacy ? __uint_as_float(a.maxbits[f]) : 0.0f;
+  const float maxv = legacy ? frame_maxv(a, f) : 0.0f;
   const int scaled = maxv > 1.0f;
   const float scale = scaled ? 1.0f / maxv : 1.0f;
 

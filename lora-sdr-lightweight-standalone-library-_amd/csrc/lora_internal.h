@@ -4,6 +4,10 @@
 
 namespace lora {
 
+// Partial maxima per frame kept in the workspace (no zeroing pass, no atomics); frames
+// longer than kMaxBpf * 4096 samples use proportionally longer blocks.
+constexpr int kMaxBpf = 80;  // SF12 frames of 66 symbols: 66 blocks of 4096 samples
+
 struct KArgs {
   const cf* iq;
   int64_t frame_len, frame_stride;
@@ -14,7 +18,8 @@ struct KArgs {
   const float* win;
   const cf* down;   // legacy dechirp table, `step` entries
   const cf* down1;  // API per-symbol down-chirp, N entries
-  const uint32_t* maxbits;
+  const uint32_t* maxbits;  // LEGACY: per-frame partial maxima [frame][mx_bpf] (float bits)
+  int mx_bpf;               // partials per frame; 0 = none (empty frames -> max 0)
   lora::FrameParams* fp;
   uint16_t* syms;
   int64_t sym_stride;
@@ -25,6 +30,13 @@ struct KArgs {
   int est_only;  // lora_estimate_offsets_batch: all symbols, raw samples, outputs only
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), 0 in production
 };
+
+// LoRaDemod.cpp:59-67 max_amp of frame f from k_frame_max's partials.
+__device__ __forceinline__ float frame_maxv(const KArgs& a, int64_t f) {
+  float m = 0.0f;
+  for (int c = 0; c < a.mx_bpf; ++c) m = fmaxf(m, __uint_as_float(a.maxbits[f * a.mx_bpf + c]));
+  return m;
+}
 
 // Fast symbol demodulator (lora_demod_fast.hip): register-blocked kissfft-exact FFT.
 // Returns false if the configuration is not covered (caller uses the generic kernel).
