@@ -6,13 +6,13 @@ current torch stream.  Host-side coding helpers (Hamming, Gray, interleave,
 whitening, CRC) are in :mod:`lora_phy_amd.codes`; the phy.hpp-style functional API
 is in :mod:`lora_phy_amd.phy`.
 """
-from . import _capi, codes, phy, shard  # noqa: F401
+from . import _capi, codes, iq_io, phy, shard  # noqa: F401
 from ._capi import LoraError
 from .demod import DemodPlan, DemodResult, LoRaDemod, compensate_offsets
 from .mod import LoRaMod, modulate
 
 __all__ = ["DemodPlan", "DemodResult", "LoRaDemod", "LoRaMod", "LoraError", "modulate",
-           "compensate_offsets", "codes", "phy", "shard", "lib_path", "version"]
+           "compensate_offsets", "codes", "iq_io", "phy", "shard", "lib_path", "version"]
 
 
 def lib_path() -> str:

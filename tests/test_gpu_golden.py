@@ -150,3 +150,14 @@ def test_capture_excerpt_gpu(G, amd):
         plan = amd.DemodPlan(7, rec["osr"], 125000, "hann" if rec["hann"] else "none",
                              dechirp=rec["dechirp"])
         check_frame(plan.run(xt), 0, rec)
+
+
+def test_capture_file_streamed_to_gpu(G, amd):
+    """iq_io streams the reference's capture excerpt into HBM; GPU demod equals the
+    reference's output for the raw osr-1 case."""
+    from lora_phy_amd import iq_io
+
+    cap = G["capture"]
+    x = iq_io.read_iq(os.path.join(GOLD, cap["file"]), device="cuda", slice_samples=4096)
+    rec = [r for r in cap["cases"] if r["osr"] == 1 and not r["dechirp"] and not r["hann"]][0]
+    check_frame(amd.DemodPlan(7).run(x), 0, rec)
