@@ -228,15 +228,33 @@ def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=2.0):
                       f"on 1 thread; demod_only: input dechirped beforehand"}
 
 
-def load_pmc(workload):
+def load_pmc(workload, key="hbm_bytes_per_launch"):
     p = os.path.join(REPO, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
-        return d.get(workload, {}).get("hbm_bytes_per_launch")
+        return d.get(workload, {}).get(key)
     except Exception:
         return None
+
+
+def valu_roofline(workload, kernel_ms):
+    """The demod kernel's real limit: VALU issue.  Counts from the committed PMC profile
+    (profiles/pmc_summary.json, same kernel and workload) against the live kernel time;
+    peak = the time the profiled fp32/fp64 instruction mix needs at the chip's measured
+    issue rates (tools/micro/pk_rate)."""
+    v = load_pmc(workload, "valu_winstr_per_launch")
+    need = load_pmc(workload, "valu_mix_ns_cu")
+    if not v or not need or not kernel_ms:
+        return None
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    achieved = v / (kernel_ms * 1e6) / ncu  # wave-instructions per ns per CU
+    return {"bound": "valu-issue", "winstr_per_launch": v,
+            "fp64_class_per_launch": load_pmc(workload, "valu_fp64_class_per_launch"),
+            "achieved_winstr_per_ns_per_cu": achieved,
+            "frac": need / ncu / (kernel_ms * 1e6),
+            "note": "frac = (profiled instruction mix at measured peak issue rates) / live kernel time"}
 
 
 def main():
@@ -276,6 +294,8 @@ def main():
         extra["sf12"] = {k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host")}
         extra["sf12"]["value_all_ranks_msym_s"] = r12["msym_s_all_ranks"]
         extra["sf12"]["roofline_frac"] = r12["dominant_gbs"] / HBM_PEAK_GBS
+        extra["sf12"]["traffic"] = load_pmc("sf12")
+        extra["sf12"]["valu"] = valu_roofline("sf12", r12["stage_ms"][2])
         del r12
         torch.cuda.empty_cache()
     if not args.no_channels and not args.sf12_only:
@@ -314,7 +334,8 @@ def main():
                          "achieved": r7["dominant_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": r7["dominant_gbs"] / HBM_PEAK_GBS,
                          "bytes_per_launch": r7["dominant_bytes_per_launch"],
-                         "traffic": load_pmc("sf7")},
+                         "traffic": load_pmc("sf7"),
+                         "valu": valu_roofline("sf7", r7["stage_ms"][2])},
             "cpu_baseline": cpu,
             "extra": extra,
         }

@@ -100,6 +100,33 @@ def main():
             if k.startswith("k_demod"):
                 summary[wl] = {"kernel": k, "fetch_size_kb": fk, "write_size_kb": wk,
                                "hbm_bytes_per_launch": hbm}
+    # VALU issue: dynamic instruction counts of the demod kernel (SQ_INSTS_VALU etc.) and
+    # the chip's measured issue rates (tools/micro/pk_rate: scalar fp32 vs fp64 / packed)
+    rates = {}
+    try:
+        for line in open(os.path.join(src, "valu_rates.txt")):
+            m = re.match(r"mode (\d): .* ([0-9.]+) wave-instr per CU per ns", line)
+            if m:
+                rates[int(m.group(1))] = float(m.group(2))
+    except OSError:
+        pass
+    for wl, tag in (("sf7", "nosf12"), ("sf12", "sf12only")):
+        v = pmc(os.path.join(src, f"pmc_VALU{tag}", "run_counter_collection.csv"))
+        for k, d in v.items():
+            if k.startswith("k_demod") and wl in summary and "SQ_INSTS_VALU" in d:
+                avg = {c: sum(x) / len(x) for c, x in d.items()}
+                dp = sum(avg.get(c, 0.0) for c in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                    "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_CVT"))
+                sp = avg["SQ_INSTS_VALU"] - dp
+                summary[wl]["valu_winstr_per_launch"] = avg["SQ_INSTS_VALU"]
+                summary[wl]["valu_fp64_class_per_launch"] = dp
+                if 0 in rates and 3 in rates:
+                    # time (ns*CU) the mix needs at the measured issue rates
+                    summary[wl]["valu_mix_ns_cu"] = sp / rates[0] + dp / rates[3]
+                    summary[wl]["valu_rate_scalar_fp32"] = rates[0]
+                    summary[wl]["valu_rate_fp64"] = rates[3]
+                plines.append(f"{wl}: {avg['SQ_INSTS_VALU']:.4g} VALU wave-instructions per launch, "
+                              f"{dp:.4g} of them fp64-class (fma/mul/add f64, conversions)")
     sf = {"sf7": 7, "sf12": 12}
     for wl, d in summary.items():
         algo = 15625 * 64 * (8 * (1 << sf[wl]) + 2)
