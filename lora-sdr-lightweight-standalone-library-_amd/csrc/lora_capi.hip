@@ -13,7 +13,8 @@
 //                CFO rotation (glibc-faithful sincosf) -> (window) -> LDS radix-4/2
 //                DIT FFT with kissfft's butterflies -> lowest-index argmax |X|^2
 //                (LoRaDemod.cpp:141-174, LoRaDetector.hpp:39-58).
-// A fused single-pass kernel for short frames lives in lora_fused.hip.
+// The register-blocked fast kernels that replace k_estimate / k_demod wherever they
+// cover the configuration live in lora_demod_fast.hip.
 //
 // All fp32 arithmetic follows the reference's operation order without contraction
 // (compiled with -ffp-contract=off, see lora_device.h), so outputs are bit-identical

@@ -398,8 +398,18 @@ __device__ __forceinline__ uint64_t symbol_key(uint64_t key, int tid, uint64_t* 
 // ABL: profiling-only ablation mask (LORA_MI355X_ABLATE; results are NOT valid):
 // 1 = identity rotation instead of sincosf, 2 = skip the pass-1 FFT stages, 4 = skip
 // the HBM loads.
+// Register budget: SF7 and SF9 are capped at 4 waves per SIMD (<= 128 VGPRs, 12-44 B of
+// spill), measured 4-5 % faster at SF7 than the compiler's 147-VGPR / 3-wave choice.
+// Elsewhere the cap spills 84-640 B (SF4-6, 8) or slowed the kernel (SF12: 11 %), so
+// those keep the compiler's budget.  tools/exp/waves_ab.sh.
+template <int SF>
+constexpr int demod_waves_per_eu() {
+  return (SF == 7 || SF == 9) ? 4 : 1;
+}
+
 template <int SF, int MODE, int ABL = 0>
-__global__ void __launch_bounds__(256) k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
+k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
   constexpr bool RAW = MODE == 3;

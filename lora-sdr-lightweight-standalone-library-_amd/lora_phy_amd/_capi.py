@@ -9,7 +9,9 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "liblora_mi355x.so")
+# LORA_MI355X_LIB: development A/B of an alternative in-tree build of the same library.
+LIB_PATH = os.environ.get("LORA_MI355X_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                             "liblora_mi355x.so")
 
 LORA_OK = 0
 LORA_EIO = -5
