@@ -635,11 +635,14 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   const int step = N * (int)p.osr;
   const float bws = bw_scale_of(p.bw_hz);
   // kissfft.hh:24-29 twiddles; LoRaDemod.cpp:17-25 window; genChirp down-chirps.
-  std::vector<std::complex<float>> tw(N), down(step), down1(N);
+  // The dechirp table holds two periods (2 * step entries) so that a symbol window
+  // starting at table phase cg reads down[cg + i*osr] without a per-sample wrap.
+  std::vector<std::complex<float>> tw(N), down(2 * (size_t)step), down1(N);
   const float phinc = -2 * std::acos((float)-1) / N;
   for (int i = 0; i < N; ++i) tw[i] = std::exp(std::complex<float>(0, i * phinc));
   float ph = 0.0f;
   host_gen_chirp(down.data(), N, (int)p.osr, step, 0.0f, true, 1.0f, ph, bws);
+  for (int i = 0; i < step; ++i) down[step + i] = down[i];
   ph = 0.0f;
   host_gen_chirp(down1.data(), N, 1, N, 0.0f, true, 1.0f, ph, bws);
   std::vector<float> win(N);
@@ -653,7 +656,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   for (int r : fft_radices(N))
     if (r != 2 && r != 4) return set_error(LORA_EINVAL, "unexpected FFT radix");
 
-  const size_t b_tw = sizeof(cf) * N, b_down = sizeof(cf) * step, b_down1 = sizeof(cf) * N,
+  const size_t b_tw = sizeof(cf) * N, b_down = sizeof(cf) * 2 * step, b_down1 = sizeof(cf) * N,
                b_win = sizeof(float) * N, b_rev = sizeof(uint16_t) * N;
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
   const size_t total = al(b_tw) + al(b_down) + al(b_down1) + al(b_win) + al(b_rev);

@@ -240,25 +240,26 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
                                               float scale, cf* in) {
   using G = Geo<SF>;
   constexpr int T = G::T, P = G::P;
+  // One per-lane base pointer per stream; the points are then at compile-time offsets
+  // T*q (times osr) from it, which fold into the loads' immediate offsets at osr 1.
+  const cf* __restrict__ xl = x + (int64_t)l * osr;
 #pragma unroll
   for (int q = 0; q < P; ++q) {
-    const int i = l + T * q;
     if (ABL & 4)
       in[q] = cf{0.0f, 0.0f};
     else
-      in[q] = x[(int64_t)i * osr];
+      in[q] = xl[(int64_t)(T * q) * osr];
   }
   if (kind == 2) {
+    const cf* __restrict__ dl = a.down1 + l;
 #pragma unroll
-    for (int q = 0; q < P; ++q) in[q] = cmul(in[q], a.down1[l + T * q]);
+    for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[T * q]);
   } else if (kind == 1) {
     if (dech) {
+      // caller-side dechirp phase cg + i*osr < 2*step: the doubled table needs no wrap
+      const cf* __restrict__ dl = a.down + cg + l * osr;
 #pragma unroll
-      for (int q = 0; q < P; ++q) {
-        int d = cg + (l + T * q) * osr;
-        if (d >= step) d -= step;
-        in[q] = cmul(in[q], a.down[d]);
-      }
+      for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[(T * q) * osr]);
     }
 #pragma unroll
     for (int q = 0; q < P; ++q) in[q] = cscale(in[q], scale);

@@ -16,7 +16,7 @@ struct KArgs {
   const cf* tw;
   const uint16_t* rev;
   const float* win;
-  const cf* down;   // legacy dechirp table, `step` entries
+  const cf* down;   // legacy dechirp table, `step` entries stored twice (2*step, no wrap)
   const cf* down1;  // API per-symbol down-chirp, N entries
   const uint32_t* maxbits;  // LEGACY: per-frame partial maxima [frame][mx_bpf] (float bits)
   int mx_bpf;               // partials per frame; 0 = none (empty frames -> max 0)
