@@ -4,14 +4,13 @@
 // points each (SF <= 5: one lane holds the whole symbol).  A 256-thread workgroup
 // handles SPW = 256/T symbols.  When T <= 64 every symbol lives inside one wave and
 // the wave works alone (wave-local LDS rows, no workgroup barrier).
-//   phase 0  slot table: (frame, symbol) of every slot, window base with the t_off
-//            rule (LoRaDemod.cpp:142-149), rotation start phase (:151-152).
-//   phase 1  coalesced 16-byte loads of each symbol window; LEGACY caller-side
-//            dechirp (e2e_chain_test.cpp:88-93) and normalisation (LoRaDemod.cpp:
-//            68-77) are applied here, once per sample, into an LDS row.
-//   pass 1   each lane gathers its 16 points (stride T), applies the CFO rotation
-//            with glibc-faithful sincosf (LoRaDemod.cpp:153-157) and the window, and
-//            runs the innermost FFT stages (radix-2 for odd SF, then radix-4) in
+//   gather   each lane loads its 16 points (stride T) straight from HBM (coalesced 8-B
+//            lanes, compile-time offsets from one base pointer), applies the LEGACY
+//            caller-side dechirp (e2e_chain_test.cpp:88-93, doubled table: no wrap) and
+//            the normalisation (LoRaDemod.cpp:68-77), the window base following the
+//            t_off rule (LoRaDemod.cpp:142-149).
+//   pass 1   CFO rotation with glibc-faithful sincosf (LoRaDemod.cpp:151-157), window,
+//            and the innermost FFT stages (radix-2 for odd SF, then radix-4) in
 //            registers.
 //   pass A/B the remaining radix-4 stages in registers after LDS transposes.
 //   argmax   over the lane's bins, then across the symbol's T lanes (lowest index
@@ -25,6 +24,16 @@
 
 namespace lora {
 namespace {
+
+// Scalar fp32 only: packed v_pk_mul/add_f32 issue at about half the scalar rate on this
+// chip (tools/micro/pk_rate) and need operand-pairing moves, so for these VALU-bound
+// kernels the scalar forms are cheaper (measured: SF7 demod -7 %, SF12 demod -13 %;
+// tools/exp/variant_ab.sh).  Same IEEE operations either way, so results are unchanged.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LORA_SCALAR_FP32 __attribute__((target("no-packed-fp32-ops")))
+#else
+#define LORA_SCALAR_FP32  // a device code-generation attribute; nothing on the host pass
+#endif
 
 template <int SF>
 struct Geo {
@@ -410,7 +419,7 @@ constexpr int demod_waves_per_eu() {
 
 template <int SF, int MODE, int ABL = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
-k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
+LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
   constexpr bool RAW = MODE == 3;
@@ -461,7 +470,7 @@ k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
 // ILP, so the register budget is capped at two waves per SIMD.
 template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-k_est_fast(KArgs a, int64_t frames, int rowc) {
+LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
   constexpr int SPB = (T >= 64 ? 256 : 64) / T;  // frames per block (block = max(T, 64))
