@@ -141,13 +141,26 @@ __device__ __forceinline__ void block_sync() {
 
 // In-register DIT stages over x[0..R): positions base + MA*u, group offset k < MA.
 // Radix-2 (optional, only with MA == 1) then radix-4 stages, as kf_work unwinds.
-template <int R, bool R2, int N, int MA>
+#ifndef LORA_UNIT_TW
+#define LORA_UNIT_TW 1
+#endif
+// UNIT (argmax-only transforms with k == 0): the butterflies whose twiddles are all
+// tw[0] = (1, 0) skip the multiplies.  x*(1,0) = (a*1 - b*0, a*0 + b*1) equals x except
+// for the sign of a zero component, and a zero's sign never reaches a non-zero result
+// or |X|^2, so every bin magnitude - hence the argmax - is bit-identical.  Transforms
+// whose bin values are used (the estimate's phase) keep the multiplies.
+template <int R, bool R2, int N, int MA, bool UNIT = false>
 __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ tw) {
   int S = 1;
   if constexpr (R2) {
     constexpr int fs = N / (2 * MA);
 #pragma unroll
-    for (int b = 0; b < R; b += 2) bfly2(x[b], x[b + 1], tw[k * fs]);
+    for (int b = 0; b < R; b += 2) {
+      if (UNIT)
+        bfly2_unit(x[b], x[b + 1]);
+      else
+        bfly2(x[b], x[b + 1], tw[k * fs]);
+    }
     S = 2;
   }
 #pragma unroll
@@ -158,8 +171,11 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ t
 #pragma unroll
       for (int uu = 0; uu < S; ++uu) {
         const int kk = k + MA * uu;
-        bfly4(x[blk + uu], x[blk + uu + S], x[blk + uu + 2 * S], x[blk + uu + 3 * S], tw[kk * fs],
-              tw[2 * kk * fs], tw[3 * kk * fs]);
+        if (UNIT && uu == 0)
+          bfly4_unit(x[blk], x[blk + S], x[blk + 2 * S], x[blk + 3 * S]);
+        else
+          bfly4(x[blk + uu], x[blk + uu + S], x[blk + uu + 2 * S], x[blk + uu + 3 * S], tw[kk * fs],
+                tw[2 * kk * fs], tw[3 * kk * fs]);
       }
     }
   }
@@ -333,7 +349,7 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
   constexpr bool WL = G::WAVE_LOCAL;
   if (!(ABL & 2)) {
 #pragma unroll
-    for (int h = 0; h < G::G1; ++h) pass_regs<R1, G::R2FIRST, N, 1>(z + h * R1, 0, a.tw);
+    for (int h = 0; h < G::G1; ++h) pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP>(z + h * R1, 0, a.tw);
   }
   uint64_t key = 0;
   if constexpr (G::NPASS == 1) {
@@ -408,13 +424,14 @@ __device__ __forceinline__ uint64_t symbol_key(uint64_t key, int tid, uint64_t* 
 // ABL: profiling-only ablation mask (LORA_MI355X_ABLATE; results are NOT valid):
 // 1 = identity rotation instead of sincosf, 2 = skip the pass-1 FFT stages, 4 = skip
 // the HBM loads.
-// Register budget: SF7 and SF9 are capped at 4 waves per SIMD (<= 128 VGPRs, 12-44 B of
-// spill), measured 4-5 % faster at SF7 than the compiler's 147-VGPR / 3-wave choice.
-// Elsewhere the cap spills 84-640 B (SF4-6, 8) or slowed the kernel (SF12: 11 %), so
-// those keep the compiler's budget.  tools/exp/waves_ab.sh.
+// Register budget: 4 waves per SIMD (<= 128 VGPRs) for SF >= 6 - the LDS rows allow
+// 4 workgroups per CU, so this is the occupancy ceiling.  With scalar fp32 the kernels
+// need 115-128 VGPRs and fit without spilling; SF <= 5 keeps a whole symbol per lane
+// (P = N complex values) and is left to the compiler.  (Under packed fp32 the SF7 cap
+// alone was worth 4-5 %, tools/exp/variant_ab.sh.)
 template <int SF>
 constexpr int demod_waves_per_eu() {
-  return (SF == 7 || SF == 9) ? 4 : 1;
+  return SF >= 6 ? 4 : 1;
 }
 
 template <int SF, int MODE, int ABL = 0>

@@ -52,6 +52,27 @@ __device__ __forceinline__ void bfly4(cf& f0, cf& f1, cf& f2, cf& f3, cf w1, cf 
   f3 = csub(s5, s4);
 }
 
+// bfly4 with w1 = w2 = w3 = (1, 0), the multiplies skipped: identical outputs up to
+// the sign of zero components (argmax-only callers, see pass_regs).
+__device__ __forceinline__ void bfly4_unit(cf& f0, cf& f1, cf& f2, cf& f3) {
+  const cf s5 = csub(f0, f2);
+  const cf a0 = cadd(f0, f2);
+  const cf s3 = cadd(f1, f3);
+  cf s4 = csub(f1, f3);
+  s4 = cf{s4.im, -s4.re};
+  f2 = csub(a0, s3);
+  f0 = cadd(a0, s3);
+  f1 = cadd(s5, s4);
+  f3 = csub(s5, s4);
+}
+
+// bfly2 with w = (1, 0), the multiply skipped (argmax-only callers, see bfly4_unit).
+__device__ __forceinline__ void bfly2_unit(cf& f0, cf& f1) {
+  const cf a = f0, t = f1;
+  f1 = csub(a, t);
+  f0 = cadd(a, t);
+}
+
 // kissfft.hh:155-162 kf_bfly2 (forward).
 __device__ __forceinline__ void bfly2(cf& f0, cf& f1, cf w) {
   const cf t = cmul(f1, w);
