@@ -189,13 +189,14 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=2.0):
+def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=10.0):
     """The reference's own lora_demodulate (oracle/_ref, compiled from the reference's
     sources, travels with the snapshot) on `threads` host cores over a bounded sample of
     the same frames; falls back to the restatement (oracle/lora_oracle.cpp) if absent.
     Reported `value`: all threads, caller-side dechirp + lora_demodulate (the GPU
     workload).  Also: one core, and demod only (input dechirped beforehand), per
-    SURVEY.md 8d.  Each leg: whole passes over the sample until `time_budget_s`."""
+    SURVEY.md 8d.  The reported leg: whole passes over the sample until `time_budget_s`
+    (about 10 s of CPU work); the single-core and demod-only legs: half that."""
     from oracle.pyoracle import Oracle, Reference
 
     if Reference.available():
@@ -205,22 +206,22 @@ def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=2.0):
     F = min(iq_dev.shape[0], max_frames)
     x = iq_dev[:F].cpu().numpy()
 
-    def rate(xs, nthreads, dechirp):
+    def rate(xs, nthreads, dechirp, budget):
         impl.demod_frames(xs[: min(len(xs), 4 * nthreads)], sf, 1, False, dechirp=dechirp, threads=nthreads)
         t0 = time.perf_counter()
         done = 0
         while True:
             impl.demod_frames(xs, sf, 1, False, dechirp=dechirp, threads=nthreads)
             done += len(xs)
-            if time.perf_counter() - t0 > time_budget_s:
+            if time.perf_counter() - t0 > budget:
                 break
         dt = time.perf_counter() - t0
         return done * data_syms / dt / 1e6, done, dt
 
-    all_rate, done, dt = rate(x, threads, True)
-    one_rate, _, _ = rate(x[: max(1, F // max(threads, 1))], 1, True)
+    all_rate, done, dt = rate(x, threads, True, time_budget_s)
+    one_rate, _, _ = rate(x[: max(1, F // max(threads, 1))], 1, True, time_budget_s / 2)
     xd = Oracle().dechirp(x.reshape(-1), sf).reshape(x.shape)  # same fp32 products as the caller loop
-    demod_only, _, _ = rate(xd, threads, False)
+    demod_only, _, _ = rate(xd, threads, False, time_budget_s / 2)
     return {"value": all_rate, "unit": "Msymbols/s", "cores": threads, "kind": kind,
             "single_core": one_rate, "demod_only_all_cores": demod_only, "cpu_model": _cpu_model(),
             "sample": f"{done} frames of the SF{sf} bench batch ({data_syms}+2 symbols each), "
