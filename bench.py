@@ -78,10 +78,13 @@ def make_input(sf, frames, data_syms, seed, device, snr_db=None):
     return syms, iq
 
 
-def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=None):
+def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=None, precision="exact",
+               inputs=None):
     N = 1 << sf
-    syms, iq = make_input(sf, frames, data_syms, 20251015 + rank, device, snr_db)
-    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device)
+    syms, iq = inputs if inputs is not None else make_input(sf, frames, data_syms, 20251015 + rank, device,
+                                                            snr_db)
+    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device,
+                         precision=precision)
     out = None
     for _ in range(warmup):
         out = plan.run(iq, out)
@@ -130,7 +133,7 @@ def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=
         "dominant_kernel": "k_demod", "dominant_gbs": dom_gbs,
         "dominant_bytes_per_launch": demod_bytes,
         "pipeline_gbs": pipe_bytes / (ms_step * 1e-3) / 1e9,
-        "iq_host": None, "plan": plan, "iq": iq,
+        "iq_host": None, "plan": plan, "iq": iq, "syms": syms,
     }
 
 
@@ -229,6 +232,35 @@ def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=10.0)
                       f"on 1 thread; demod_only: input dechirped beforehand"}
 
 
+def fast_summary(r):
+    """LORA_PRECISION_FAST line (hardware sin/cos rotation; stated tolerance in
+    include/lora_mi355x.h): same workload and inputs as the exact run."""
+    return {"precision": "fast", "ms_per_step": r["ms_per_step"], "stage_ms": r["stage_ms"],
+            "symbols_ok": r["symbols_ok"], "value_all_ranks_msym_s": r["msym_s_all_ranks"],
+            "demod_gbs": r["dominant_gbs"], "demod_roofline_frac": r["dominant_gbs"] / HBM_PEAK_GBS}
+
+
+def hbm_probe(device, nbytes=2 << 30, reps=5):
+    """SURVEY.md 8d cross-check: device-to-device copy bandwidth on the same GPU
+    (bytes read + bytes written per second), the chip's achievable HBM rate next to the
+    8 TB/s spec."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize(device)
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    t1.record()
+    torch.cuda.synchronize(device)
+    gbs = 2 * nbytes * reps / (t0.elapsed_time(t1) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return gbs
+
+
 def load_pmc(workload, key="hbm_bytes_per_launch"):
     p = os.path.join(REPO, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
@@ -270,6 +302,7 @@ def main():
     ap.add_argument("--sf12-only", action="store_true", help="profiling: SF12 workload only")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-channels", action="store_true", help="skip the configs[4] measurement")
+    ap.add_argument("--no-fast", action="store_true", help="skip the LORA_PRECISION_FAST lines")
     ap.add_argument("--channel-frames", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--sync", type=lambda v: int(v, 0), default=0x12,
@@ -285,24 +318,40 @@ def main():
         r12 = run_config(12, args.sf12_frames, args.data_symbols, args.steps, args.warmup, rank, dist,
                          device)
         if rank == 0:
-            print(json.dumps({k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host")}))
+            print(json.dumps({k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host", "syms")}))
         return
     r7 = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, rank, dist, device)
     extra = {}
+    if not args.no_fast:
+        r7f = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, rank, dist, device,
+                         precision="fast", inputs=(r7["syms"], r7["iq"]))
+        extra["fast_rotation_sf7"] = fast_summary(r7f)
+        del r7f
     if not args.no_sf12:
         r12 = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2),
                          args.warmup, rank, dist, device)
-        extra["sf12"] = {k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host")}
+        extra["sf12"] = {k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host", "syms")}
         extra["sf12"]["value_all_ranks_msym_s"] = r12["msym_s_all_ranks"]
         extra["sf12"]["roofline_frac"] = r12["dominant_gbs"] / HBM_PEAK_GBS
         extra["sf12"]["traffic"] = load_pmc("sf12")
         extra["sf12"]["valu"] = valu_roofline("sf12", r12["stage_ms"][2])
+        extra["sf12"]["frame_max_read_gbs"] = r12["iq_bytes"] / (r12["stage_ms"][0] * 1e-3) / 1e9
+        if not args.no_fast:
+            r12f = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2), args.warmup, rank,
+                              dist, device, precision="fast", inputs=(r12["syms"], r12["iq"]))
+            extra["fast_rotation_sf12"] = fast_summary(r12f)
+            del r12f
         del r12
         torch.cuda.empty_cache()
     if not args.no_channels and not args.sf12_only:
         extra["channels"] = run_channels(args.channel_frames, 16, max(args.steps // 4, 2), 1, rank, dist,
                                          device)
         torch.cuda.empty_cache()
+    probe = None
+    try:
+        probe = hbm_probe(device)
+    except Exception as e:  # a probe must not kill the measurement
+        log("hbm probe failed:", e)
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
         try:
@@ -336,7 +385,11 @@ def main():
                          "frac": r7["dominant_gbs"] / HBM_PEAK_GBS,
                          "bytes_per_launch": r7["dominant_bytes_per_launch"],
                          "traffic": load_pmc("sf7"),
-                         "valu": valu_roofline("sf7", r7["stage_ms"][2])},
+                         "valu": valu_roofline("sf7", r7["stage_ms"][2]),
+                         "hbm_probe": {"d2d_copy_gbs": probe,
+                                       "frame_max_read_gbs": r7["iq_bytes"] / (r7["stage_ms"][0] * 1e-3) / 1e9,
+                                       "note": "achievable rates on this GPU: torch D2D copy (read+write) and "
+                                               "the k_frame_max streaming read of the same IQ"}},
             "cpu_baseline": cpu,
             "extra": extra,
         }

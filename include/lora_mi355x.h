@@ -68,6 +68,20 @@ extern "C" {
  *   reference's Python AWGN sweep (tests/awgn_sweep.py:262-265). */
 #define LORA_MODE_RAW 2
 
+/* Rotation arithmetic of the symbol demod (lora_demod_batch, LEGACY / API modes).
+ * EXACT: bit-identical to the reference (glibc sincosf per sample, LoRaDemod.cpp:151-157;
+ *   every output equals lora_demodulate's).  The default.
+ * FAST: the per-sample CFO rotation uses the hardware sine/cosine (v_sin/v_cos_f32 on
+ *   the phase in revolutions, absolute phase error ~1e-5 rad) instead of glibc's
+ *   double-precision polynomial.  The normalisation, the offset estimate (cfo,
+ *   time_offset) and the sync word stay exact; data symbol indices equal the reference
+ *   except where two FFT bins are within rounding of each other (near-ties under
+ *   noise).  Stated tolerance, checked by tests/test_gpu_fast_rotation.py: identical
+ *   symbols on noiseless and >= 0 dB frames; >= 99 % per-symbol agreement at -10 dB
+ *   SF7, and SER within 0.01 absolute of the exact path at any SNR. */
+#define LORA_PRECISION_EXACT 0
+#define LORA_PRECISION_FAST 1
+
 typedef struct lora_demod_plan lora_demod_plan;
 
 typedef struct {
@@ -80,6 +94,7 @@ typedef struct {
                      (e2e_chain_test.cpp:85-93); 0 = input already dechirped */
   int mode;       /* LORA_MODE_* */
   int device;     /* HIP device ordinal */
+  int precision;  /* LORA_PRECISION_* (0 = EXACT) */
 } lora_demod_params;
 
 /* Per-frame outputs; any pointer may be NULL.  Device pointers. */

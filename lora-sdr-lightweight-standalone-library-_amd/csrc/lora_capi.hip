@@ -630,6 +630,8 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
     return set_error(LORA_EINVAL, "bad window");
   if (p.mode != LORA_MODE_LEGACY && p.mode != LORA_MODE_API && p.mode != LORA_MODE_RAW)
     return set_error(LORA_EINVAL, "bad mode");
+  if (p.precision != LORA_PRECISION_EXACT && p.precision != LORA_PRECISION_FAST)
+    return set_error(LORA_EINVAL, "bad precision");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (p.device < 0 || p.device >= ndev) return set_error(LORA_EINVAL, "bad device ordinal");
@@ -841,6 +843,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.max_amp = out->max_amp;
   a.est_only = 0;
   a.ablate = plan->ablate;
+  a.fast_rot = (p.precision == LORA_PRECISION_FAST && p.mode != LORA_MODE_RAW) ? 1 : 0;
 
   const int s0 = a.have_sync ? 2 : 0;
   const int64_t per = total - s0;

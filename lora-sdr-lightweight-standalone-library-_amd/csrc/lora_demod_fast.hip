@@ -283,8 +283,14 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
     if (dech) {
       // caller-side dechirp phase cg + i*osr < 2*step: the doubled table needs no wrap
       const cf* __restrict__ dl = a.down + cg + l * osr;
+      if (ABL & 8) {  // profiling only: one table value for every point
+        const cf d0 = dl[0];
 #pragma unroll
-      for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[(T * q) * osr]);
+        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], d0);
+      } else {
+#pragma unroll
+        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[(T * q) * osr]);
+      }
     }
 #pragma unroll
     for (int q = 0; q < P; ++q) in[q] = cscale(in[q], scale);
@@ -293,11 +299,26 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 
 // CFO rotation (glibc-faithful sincosf, LoRaDemod.cpp:151-157) when ROT, window
 // (:158-160), and placement in pass-1 leaf order.
-template <int SF, bool ROT, int ABL>
+template <int SF, bool ROT, int ABL, bool FAST = false>
 __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, float rate,
                                              bool hann, const float* __restrict__ win, int l) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
+  if constexpr (FAST && ROT && !(ABL & 1)) {
+    // LORA_PRECISION_FAST: the same fp32 phase (LoRaDemod.cpp:151-154), then the hardware
+    // sine/cosine on its fractional revolution (v_fract, v_sin_f32, v_cos_f32) instead of
+    // glibc's sincosf - not bit-exact (include/lora_mi355x.h states the tolerance).
+    constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const float ph = start + rate * (float)(l + T * q);
+      const float rev = __builtin_amdgcn_fractf(ph * INV_2PI);
+      cf v = cmul(in[q], cf{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)});
+      if (hann) v = cscale(v, win[l + T * q]);
+      z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
+    }
+    return;
+  }
   if (!ROT || (ABL & 1)) {
 #pragma unroll
     for (int q = 0; q < P; ++q) {
@@ -423,7 +444,7 @@ __device__ __forceinline__ uint64_t symbol_key(uint64_t key, int tid, uint64_t* 
 //         time; MODE 3: RAW (detector only: no normalisation, estimate or rotation).
 // ABL: profiling-only ablation mask (LORA_MI355X_ABLATE; results are NOT valid):
 // 1 = identity rotation instead of sincosf, 2 = skip the pass-1 FFT stages, 4 = skip
-// the HBM loads.
+// the HBM loads, 8 = one dechirp-table value per lane instead of one per point.
 // Register budget: 4 waves per SIMD (<= 128 VGPRs) for SF >= 6 - the LDS rows allow
 // 4 workgroups per CU, so this is the occupancy ceiling.  With scalar fp32 the kernels
 // need 115-128 VGPRs and fit without spilling; SF <= 5 keeps a whole symbol per lane
@@ -434,7 +455,7 @@ constexpr int demod_waves_per_eu() {
   return SF >= 6 ? 4 : 1;
 }
 
-template <int SF, int MODE, int ABL = 0>
+template <int SF, int MODE, int ABL = 0, bool FAST = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   using G = Geo<SF>;
@@ -470,7 +491,7 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
 
   cf in[P], z[P];
   gather_points<SF, ABL>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, scale, in);
-  rotate_place<SF, !RAW, ABL>(in, z, start, p.rate, hann, a.win, l);
+  rotate_place<SF, !RAW, ABL, FAST>(in, z, start, p.rate, hann, a.win, l);
   uint64_t key = fft_key<SF, false, ABL>(z, rows + (size_t)g * rowc, l, a);
   key = symbol_key<SF>(key, tid, red);
   if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + (s - s0)] = (uint16_t)key_index(key);
@@ -647,18 +668,18 @@ bool launch_est_sf(const KArgs& a, int64_t frames, hipStream_t st) {
   return launch_est_mode<SF, 2>(a, frames, st);
 }
 
-template <int SF, int MODE, int ABL = 0>
+template <int SF, int MODE, int ABL = 0, bool FAST = false>
 bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
   const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * (size_t)G::SPW * rowc;
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_demod_fast<SF, MODE, ABL>,
+    if (hipFuncSetAttribute((const void*)k_demod_fast<SF, MODE, ABL, FAST>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return false;
   const int64_t grid = (work + G::SPW - 1) / G::SPW;
-  hipLaunchKernelGGL((k_demod_fast<SF, MODE, ABL>), dim3((unsigned)grid), dim3(256), lds, st, a, s0, work,
+  hipLaunchKernelGGL((k_demod_fast<SF, MODE, ABL, FAST>), dim3((unsigned)grid), dim3(256), lds, st, a, s0, work,
                      rowc);
   return true;
 }
@@ -673,12 +694,21 @@ bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
         case 2: return launch_mode<SF, 0, 2>(a, s0, work, st);
         case 3: return launch_mode<SF, 0, 3>(a, s0, work, st);
         case 4: return launch_mode<SF, 0, 4>(a, s0, work, st);
+        case 5: return launch_mode<SF, 0, 5>(a, s0, work, st);
         case 7: return launch_mode<SF, 0, 7>(a, s0, work, st);
+        case 8: return launch_mode<SF, 0, 8>(a, s0, work, st);
+        case 9: return launch_mode<SF, 0, 9>(a, s0, work, st);
+        case 12: return launch_mode<SF, 0, 12>(a, s0, work, st);
         default: break;
       }
     }
   }
   if (a.mode == LORA_MODE_RAW) return launch_mode<SF, 3>(a, s0, work, st);
+  if (a.fast_rot) {  // LORA_PRECISION_FAST (include/lora_mi355x.h)
+    if (simple && a.dechirp) return launch_mode<SF, 0, 0, true>(a, s0, work, st);
+    if (simple) return launch_mode<SF, 1, 0, true>(a, s0, work, st);
+    return launch_mode<SF, 2, 0, true>(a, s0, work, st);
+  }
   if (simple && a.dechirp) return launch_mode<SF, 0>(a, s0, work, st);
   if (simple) return launch_mode<SF, 1>(a, s0, work, st);
   return launch_mode<SF, 2>(a, s0, work, st);

@@ -29,6 +29,7 @@ struct KArgs {
   float* max_amp;
   int est_only;  // lora_estimate_offsets_batch: all symbols, raw samples, outputs only
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), 0 in production
+  int fast_rot;  // LORA_PRECISION_FAST: hardware sin/cos rotation in the symbol demod
 };
 
 // LoRaDemod.cpp:59-67 max_amp of frame f from k_frame_max's partials.

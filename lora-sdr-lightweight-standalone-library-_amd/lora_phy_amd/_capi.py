@@ -51,6 +51,7 @@ class DemodParams(C.Structure):
         ("dechirp", C.c_int),
         ("mode", C.c_int),
         ("device", C.c_int),
+        ("precision", C.c_int),
     ]
 
 

@@ -18,6 +18,9 @@ from . import _capi
 _WINDOWS = {"none": _capi.LORA_WINDOW_NONE, "hann": _capi.LORA_WINDOW_HANN,
             None: _capi.LORA_WINDOW_NONE, 0: _capi.LORA_WINDOW_NONE, 1: _capi.LORA_WINDOW_HANN}
 _MODES = {"legacy": _capi.LORA_MODE_LEGACY, "api": _capi.LORA_MODE_API, "raw": _capi.LORA_MODE_RAW}
+# include/lora_mi355x.h LORA_PRECISION_*: "exact" = bit-identical to the reference
+# (default); "fast" = hardware sin/cos for the per-sample CFO rotation (stated tolerance).
+_PRECISIONS = {"exact": 0, "fast": 1}
 
 
 @dataclass
@@ -45,7 +48,7 @@ class DemodPlan:
     """A device plan for one demodulator configuration (lora_demod_init equivalent)."""
 
     def __init__(self, sf: int, osr: int = 1, bw: int = 125000, window="none",
-                 dechirp: bool = False, mode: str = "legacy", device=None):
+                 dechirp: bool = False, mode: str = "legacy", device=None, precision: str = "exact"):
         if not torch.cuda.is_available():
             raise RuntimeError("lora_phy_amd needs a HIP GPU (torch.cuda.is_available() is False)")
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else
@@ -57,9 +60,12 @@ class DemodPlan:
         self.window = window
         self.dechirp = bool(dechirp)
         self.mode = mode
+        if precision not in _PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_PRECISIONS)}")
+        self.precision = precision
         self._lib = _capi.lib()
         prm = _capi.DemodParams(self.sf, self.osr, self.bw, _WINDOWS[window], int(self.dechirp),
-                                _MODES[mode], dev.index)
+                                _MODES[mode], dev.index, _PRECISIONS[precision])
         h = C.c_void_p()
         _capi.check(self._lib.lora_demod_plan_create(C.byref(prm), C.byref(h)))
         self._h = h
@@ -154,10 +160,10 @@ class LoRaDemod:
 
     def __init__(self, sf: int, sync: int = 0x12, thresh: float = -30.0, mtu: int = 256,
                  bw: int = 125000, cr: int = 1, osr: int = 1, window="none",
-                 dechirp: bool = True, mode: str = "legacy", device=None):
+                 dechirp: bool = True, mode: str = "legacy", device=None, precision: str = "exact"):
         self.sf, self.sync, self.thresh, self.mtu = int(sf), int(sync) & 0xFF, float(thresh), int(mtu)
         self.bw, self.cr, self.osr = int(bw), int(cr), int(osr) if osr else 1
-        self.plan = DemodPlan(sf, self.osr, bw, window, dechirp, mode, device)
+        self.plan = DemodPlan(sf, self.osr, bw, window, dechirp, mode, device, precision)
         self.last: Optional[DemodResult] = None
 
     def work(self, iq: torch.Tensor) -> torch.Tensor:
