@@ -51,7 +51,7 @@ def test_version_and_error_string():
 
 
 @pytest.mark.parametrize("field,value", [("sf", 1), ("sf", 13), ("bw_hz", 100000), ("window", 7),
-                                         ("mode", 9), ("osr", 1000)])
+                                         ("mode", 9), ("osr", 1000), ("precision", 2), ("precision", -1)])
 def test_plan_create_rejects_bad_parameters(field, value):
     """Validation happens before any HIP call: -EINVAL (reference returns -1,
     phy.cpp:27-33), with a message."""
@@ -64,6 +64,16 @@ def test_plan_create_rejects_bad_parameters(field, value):
     assert lib.lora_last_error().decode()
     with pytest.raises(_capi.LoraError):
         _capi.check(rc)
+
+
+def test_param_structs_match_header():
+    """The ctypes mirrors of lora_demod_params / lora_demod_outputs list the header's
+    fields in the header's order (a drift would silently shift every field after it)."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for cname, pystruct in (("lora_demod_params", _capi.DemodParams), ("lora_demod_outputs", _capi.DemodOutputs)):
+        body = re.search(r"typedef struct \{([^}]*)\}\s*" + cname + ";", text).group(1)
+        fields = re.findall(r"(\w+)\s*;", body)
+        assert fields == [f for f, _ in pystruct._fields_], cname
 
 
 def test_null_arguments_rejected():
