@@ -107,3 +107,25 @@ def test_fast_rotation_api_mode(O, amd):
 def test_bad_precision_rejected(amd):
     with pytest.raises(ValueError):
         amd.DemodPlan(7, precision="approximate")
+
+
+@pytest.mark.parametrize("sf,osr,hann", [(8, 2, True), (9, 1, True), (7, 3, False)])
+def test_fast_rotation_generic_configurations(O, amd, sf, osr, hann):
+    """The run-time-flag kernel (osr > 1, Hann window) in FAST mode: same symbols as the
+    reference on 10 dB frames, estimate outputs bit-exact."""
+    rng = np.random.default_rng(sf * 10 + osr)
+    N, F, S = 1 << sf, 12, 10
+    frames = []
+    for f in range(F):
+        syms = rng.integers(0, N, S).astype(np.uint16)
+        x = O.lora_modulate(syms, sf, osr, 125000, 1.0, int(rng.integers(0, 256)))
+        x = (x + 0.3 * (rng.standard_normal(len(x)) + 1j * rng.standard_normal(len(x)))).astype(np.complex64)
+        frames.append(x)
+    iq = np.stack(frames)
+    plan = amd.DemodPlan(sf, osr, 125000, "hann" if hann else "none", dechirp=True, precision="fast")
+    res = plan.run(torch.from_numpy(iq).cuda())
+    osyms, osync, ocfo, otoff, cnt = O.demod_frames(iq, sf, osr, hann, dechirp=True, threads=8)
+    np.testing.assert_array_equal(res.symbols.cpu().numpy(), osyms[:, :S])
+    np.testing.assert_array_equal(res.sync.cpu().numpy(), osync)
+    np.testing.assert_array_equal(bits(res.cfo.cpu().numpy()), bits(ocfo))
+    np.testing.assert_array_equal(bits(res.time_offset.cpu().numpy()), bits(otoff))
