@@ -391,6 +391,73 @@ __global__ void __launch_bounds__(256) k_frame_max(KArgs a, int bpf, int chunk,
   }
 }
 
+// Short frames (one k_frame_max block per frame would stream less than two 4096-sample
+// batches): one wave per frame, 4 frames per 256-thread block, the same 16-byte batched
+// loads with the wave's 64 lanes striding the frame; the wave's maximum is the frame's
+// single partial (mx_bpf = 1).  configs[4]'s 18-symbol SF7 frames (2304 samples): the
+// block-per-frame pass ran at 4.9 TB/s.
+__global__ void __launch_bounds__(256) k_frame_max_wave(KArgs a, int64_t frames,
+                                                        uint32_t* __restrict__ maxbits) {
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= frames) return;  // whole waves exit together
+  const int t = threadIdx.x & 63;
+  const int64_t fb = f * a.frame_stride;
+  const cf* x = a.iq + fb;
+  const int step = a.step;
+  const int64_t len = a.frame_len;
+  float m = 0.0f;
+  if ((fb & 1) == 0) {
+    constexpr int KB = 8;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const int64_t p1 = len >> 1;
+    int d = (2 * t) % step;
+    const int inc = 128 % step;
+    for (int64_t pb = t; pb < p1; pb += (int64_t)KB * 64) {
+      f4v q[KB];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const int64_t pr = pb + (int64_t)k * 64;
+        q[k] = pr < p1 ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x + 2 * pr))
+                       : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+      if (a.dechirp) {
+        cf w0[KB], w1[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const int d1 = (d + 1 == step) ? 0 : d + 1;
+          w0[k] = a.down[d];
+          w1[k] = a.down[d1];
+          d += inc;
+          if (d >= step) d -= step;
+        }
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const cf v0 = lora::cmul(cf{q[k][0], q[k][1]}, w0[k]);
+          const cf v1 = lora::cmul(cf{q[k][2], q[k][3]}, w1[k]);
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(v0.re), fabsf(v0.im)), fmaxf(fabsf(v1.re), fabsf(v1.im))));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < KB; ++k)
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(q[k][0]), fabsf(q[k][1])), fmaxf(fabsf(q[k][2]), fabsf(q[k][3]))));
+      }
+    }
+    if ((len & 1) && t == 0) {  // odd frame length: the last sample
+      cf v = x[len - 1];
+      if (a.dechirp) v = lora::cmul(v, a.down[(len - 1) % step]);
+      m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+    }
+  } else {
+    for (int64_t j = t; j < len; j += 64) {
+      cf v = x[j];
+      if (a.dechirp) v = lora::cmul(v, a.down[j % step]);
+      m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (t == 0) maxbits[f] = __float_as_uint(m);
+}
+
 // G symbols per workgroup; work item w -> (frame, symbol) over the symbols that are
 // not sync symbols.
 __global__ void __launch_bounds__(256) k_demod(KArgs a, int G, int s0, int64_t work) {
@@ -858,6 +925,12 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   // (0.17 ms) rather than 3 x 2816 (0.185 ms, partly idle batches); SF12 66 x 4096.
   const int bpf = frame_len > 0 ? (int)std::min<int64_t>(lora::kMaxBpf, std::max<int64_t>(1, frame_len / max_chunk))
                                 : 1;
+  // frames shorter than two batches: one wave per frame (k_frame_max_wave)
+  static const bool wave_ok = [] {
+    const char* e = std::getenv("LORA_MI355X_MAXWAVE");
+    return !(e && e[0] == '0');
+  }();
+  const bool max_wave = wave_ok && bpf == 1;
   a.mx_bpf = (p.mode == LORA_MODE_LEGACY && frame_len > 0) ? bpf : 0;
   // split evenly over the frame's blocks
   const int chunk = (int)((((frame_len + bpf - 1) / bpf) + 1) & ~int64_t(1));
@@ -869,7 +942,10 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   auto prep = [&](const KArgs& ac, uint32_t* mb, int64_t nf, hipStream_t s) {
     if (p.mode == LORA_MODE_LEGACY && frame_len > 0) {
       ProfScope ps(plan, 0, s);
-      hipLaunchKernelGGL(k_frame_max, dim3((unsigned)(nf * bpf)), dim3(256), 0, s, ac, bpf, chunk, mb);
+      if (max_wave)
+        hipLaunchKernelGGL(k_frame_max_wave, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, s, ac, nf, mb);
+      else
+        hipLaunchKernelGGL(k_frame_max, dim3((unsigned)(nf * bpf)), dim3(256), 0, s, ac, bpf, chunk, mb);
     }
     ProfScope ps(plan, 1, s);
     if (!plan->use_fast || !lora::launch_est_fast(ac, nf, s))
