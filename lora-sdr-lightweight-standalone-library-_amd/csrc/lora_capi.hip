@@ -776,9 +776,9 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   if (e == hipSuccess) e = hipMemcpy(plan->rev, rev.data(), b_rev, hipMemcpyHostToDevice);
   hipSetDevice(prev);
   if (e != hipSuccess) {
-    hipFree(mem);
-    delete plan;
-    return set_error(LORA_EIO, std::string("plan table upload: ") + hipGetErrorString(e));
+    const std::string msg = std::string("plan setup: ") + hipGetErrorString(e);
+    lora_demod_plan_destroy(plan);  // streams / events created so far, and the tables
+    return set_error(LORA_EIO, msg);
   }
   *out = plan;
   return LORA_OK;
