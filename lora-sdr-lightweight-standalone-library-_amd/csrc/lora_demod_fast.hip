@@ -182,11 +182,24 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ t
 }
 
 
+// pass_regs<16, false, N, MA> with the twiddles read from the slot-major copy
+// twT[j*MA + k] (lora::twT_index): the same butterflies, operands and order.
+template <int MA>
+__device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__ twT) {
+#pragma unroll
+  for (int blk = 0; blk < 16; blk += 4)
+    bfly4(x[blk], x[blk + 1], x[blk + 2], x[blk + 3], twT[0 * MA + k], twT[1 * MA + k], twT[2 * MA + k]);
+#pragma unroll
+  for (int uu = 0; uu < 4; ++uu)
+    bfly4(x[uu], x[uu + 4], x[uu + 8], x[uu + 12], twT[(3 + 3 * uu) * MA + k], twT[(4 + 3 * uu) * MA + k],
+          twT[(5 + 3 * uu) * MA + k]);
+}
+
 // The other lanes' share of one pass: read R points from LDS, run the stages,
 // either write them back or fold them into the argmax key.
 template <int R, int N, int MA, int SF, int T, int P, bool LAST>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
-                                         uint64_t& key) {
+                                         uint64_t& key, const cf* __restrict__ twT = nullptr) {
   constexpr int NG = P / R;
 #pragma unroll
   for (int gg = 0; gg < NG; ++gg) {
@@ -196,6 +209,12 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     const cf* rb = row + lds_slot<SF>(cc * MA * R + k);  // k < MA, MA*u: disjoint bits
 #pragma unroll
     for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
+    if constexpr (SF == 12 && R == 16 && (MA == 16 || MA == 256)) {
+      if (twT) {
+        pass_regs_T<MA>(xs, k, twT);
+        continue;
+      }
+    }
     pass_regs<R, false, N, MA>(xs, k, tw);
   }
   if constexpr (LAST) {
@@ -399,11 +418,11 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
     if constexpr (G::NPASS == 2) {
       pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row, z, l, a.tw, key);
     } else {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, false>(row, z, l, a.tw, key);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, false>(row, z, l, a.tw, key, a.twT16);
       block_sync<WL>();
       write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
       block_sync<WL>();
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true>(row, z, l, a.tw, key);
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true>(row, z, l, a.tw, key, a.twT256);
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)

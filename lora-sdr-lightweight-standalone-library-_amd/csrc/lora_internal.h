@@ -30,7 +30,17 @@ struct KArgs {
   int est_only;  // lora_estimate_offsets_batch: all symbols, raw samples, outputs only
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), 0 in production
   int fast_rot;  // LORA_PRECISION_FAST: hardware sin/cos rotation in the symbol demod
+  const cf* twT16;   // SF12: slot-major twiddles of the MA = 16 / 256 LDS passes (or null)
+  const cf* twT256;
 };
+
+// Twiddle index of slot j (0..14) of a radix-16 LDS pass with butterfly group k < MA, in
+// pass_regs' order: slots 0-2 the first radix-4 stage (tw[q*k*fs1], q = 1..3, fs1 =
+// N/(4*MA)), slots 3+3*uu+(q-1) the second (kk = k + MA*uu, tw[q*kk*fs2], fs2 = fs1/4).
+__host__ __device__ constexpr int twT_index(int N, int MA, int j, int k) {
+  return j < 3 ? (j + 1) * k * (N / (4 * MA))
+               : ((j - 3) % 3 + 1) * (k + MA * ((j - 3) / 3)) * (N / (16 * MA));
+}
 
 // LoRaDemod.cpp:59-67 max_amp of frame f from k_frame_max's partials.
 __device__ __forceinline__ float frame_maxv(const KArgs& a, int64_t f) {
