@@ -635,8 +635,8 @@ struct lora_demod_plan {
   cf* down1;
   float* win;
   uint16_t* rev;
-  cf* twT16 = nullptr;   // SF12 pass-A twiddles, slot-major (15 x 16)
-  cf* twT256 = nullptr;  // SF12 pass-B twiddles, slot-major (15 x 256)
+  cf* twTA = nullptr;  // pass-A twiddles, slot-major (lora::twT_index), or null
+  cf* twTB = nullptr;  // pass-B twiddles, slot-major, or null
   int use_fast;  // 0: generic LDS kernel only (LORA_MI355X_GENERIC=1, for A/B checks)
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), results invalid
   int max_chunks;  // 2-stream pipeline depth (LORA_MI355X_CHUNKS, default 1 = off)
@@ -730,19 +730,27 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   for (int r : fft_radices(N))
     if (r != 2 && r != 4) return set_error(LORA_EINVAL, "unexpected FFT radix");
 
-  // SF12 LDS passes (radix 16, butterfly groups k < MA = 16 and 256): the 15 twiddles each
-  // group uses, stored slot-major (twT[j*MA + k] = tw[index of slot j for group k]) so one
-  // wave instruction reads MA-contiguous entries instead of a 3k-strided gather.  Copies
-  // of the same table values: results unchanged (lora::twT_index).
+  // The fast kernels' LDS passes (radix 16 or 4 over butterfly groups k < MA): the
+  // twiddles each group uses, stored slot-major (twT[j*MA + k] = tw[index of slot j for
+  // group k]) so a wave instruction reads contiguous entries instead of a k-strided
+  // gather.  Copies of the same table values: results unchanged (lora::twT_index).
   std::vector<std::complex<float>> twT;
+  int twTA_off = -1, twTB_off = -1;
   static const bool twt_ok = [] {
     const char* e = std::getenv("LORA_MI355X_TWT");
     return !(e && e[0] == '0');
   }();
-  if (p.sf == 12 && twt_ok) {
-    for (int MA : {16, 256})
-      for (int j = 0; j < 15; ++j)
+  if (twt_ok && p.sf >= 6) {
+    lora::PassShape ps = lora::pass_shape((int)p.sf);
+    auto add = [&](int R, int MA) {
+      const int off = (int)twT.size();
+      const int slots = R == 16 ? 15 : 3;
+      for (int j = 0; j < slots; ++j)
         for (int k = 0; k < MA; ++k) twT.push_back(tw[lora::twT_index(N, MA, j, k)]);
+      return off;
+    };
+    if (ps.RA > 1) twTA_off = add(ps.RA, ps.MA_A);
+    if (ps.RB > 1) twTB_off = add(ps.RB, ps.MA_B);
   }
   const size_t b_tw = sizeof(cf) * N, b_down = sizeof(cf) * 2 * step, b_down1 = sizeof(cf) * N,
                b_win = sizeof(float) * N, b_rev = sizeof(uint16_t) * N, b_twT = sizeof(cf) * twT.size();
@@ -782,8 +790,9 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   b += al(b_win);
   plan->rev = reinterpret_cast<uint16_t*>(b);
   b += al(b_rev);
-  plan->twT16 = twT.empty() ? nullptr : reinterpret_cast<cf*>(b);
-  plan->twT256 = twT.empty() ? nullptr : plan->twT16 + 15 * 16;
+  cf* twT_dev = twT.empty() ? nullptr : reinterpret_cast<cf*>(b);
+  plan->twTA = twTA_off >= 0 ? twT_dev + twTA_off : nullptr;
+  plan->twTB = twTB_off >= 0 ? twT_dev + twTB_off : nullptr;
   hipError_t e = hipStreamCreateWithFlags(&plan->aux, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->ev_fork, hipEventDisableTiming);
   for (int c = 0; c < kMaxChunks && e == hipSuccess; ++c)
@@ -793,7 +802,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   if (e == hipSuccess) e = hipMemcpy(plan->down1, down1.data(), b_down1, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->win, win.data(), b_win, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->rev, rev.data(), b_rev, hipMemcpyHostToDevice);
-  if (e == hipSuccess && !twT.empty()) e = hipMemcpy(plan->twT16, twT.data(), b_twT, hipMemcpyHostToDevice);
+  if (e == hipSuccess && !twT.empty()) e = hipMemcpy(twT_dev, twT.data(), b_twT, hipMemcpyHostToDevice);
   hipSetDevice(prev);
   if (e != hipSuccess) {
     const std::string msg = std::string("plan setup: ") + hipGetErrorString(e);
@@ -918,8 +927,8 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.win = plan->win;
   a.down = plan->down;
   a.down1 = plan->down1;
-  a.twT16 = plan->twT16;
-  a.twT256 = plan->twT256;
+  a.twTA = plan->twTA;
+  a.twTB = plan->twTB;
   unsigned char* wsb = static_cast<unsigned char*>(workspace);
   uint32_t* maxbits = reinterpret_cast<uint32_t*>(wsb);
   a.maxbits = maxbits;

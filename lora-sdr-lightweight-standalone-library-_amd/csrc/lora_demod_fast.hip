@@ -55,6 +55,12 @@ struct Geo {
   static constexpr bool WAVE_LOCAL = T <= 64;
 };
 
+static_assert(pass_shape(7).RA == Geo<7>::RA && pass_shape(7).MA_A == Geo<7>::MA_A &&
+                  pass_shape(12).RB == Geo<12>::RB && pass_shape(12).MA_B == Geo<12>::MA_B &&
+                  pass_shape(9).RB == Geo<9>::RB && pass_shape(10).MA_B == Geo<10>::MA_B &&
+                  pass_shape(6).RA == Geo<6>::RA && pass_shape(11).MA_B == Geo<11>::MA_B,
+              "host pass_shape must match the kernels' Geo");
+
 // kissfft leaf position of input v inside an R-point block (radices 4,..,4[,2]).
 constexpr int leaf_pos(int R, int v) {
   int pos = 0, rem = R;
@@ -184,15 +190,18 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ t
 
 // pass_regs<16, false, N, MA> with the twiddles read from the slot-major copy
 // twT[j*MA + k] (lora::twT_index): the same butterflies, operands and order.
-template <int MA>
+template <int R, int MA>
 __device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__ twT) {
+  static_assert(R == 4 || R == 16, "radix-4 / radix-16 passes");
 #pragma unroll
-  for (int blk = 0; blk < 16; blk += 4)
+  for (int blk = 0; blk < R; blk += 4)
     bfly4(x[blk], x[blk + 1], x[blk + 2], x[blk + 3], twT[0 * MA + k], twT[1 * MA + k], twT[2 * MA + k]);
+  if constexpr (R == 16) {
 #pragma unroll
-  for (int uu = 0; uu < 4; ++uu)
-    bfly4(x[uu], x[uu + 4], x[uu + 8], x[uu + 12], twT[(3 + 3 * uu) * MA + k], twT[(4 + 3 * uu) * MA + k],
-          twT[(5 + 3 * uu) * MA + k]);
+    for (int uu = 0; uu < 4; ++uu)
+      bfly4(x[uu], x[uu + 4], x[uu + 8], x[uu + 12], twT[(3 + 3 * uu) * MA + k], twT[(4 + 3 * uu) * MA + k],
+            twT[(5 + 3 * uu) * MA + k]);
+  }
 }
 
 // The other lanes' share of one pass: read R points from LDS, run the stages,
@@ -209,9 +218,9 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     const cf* rb = row + lds_slot<SF>(cc * MA * R + k);  // k < MA, MA*u: disjoint bits
 #pragma unroll
     for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
-    if constexpr (SF == 12 && R == 16 && (MA == 16 || MA == 256)) {
+    if constexpr (R == 4 || R == 16) {
       if (twT) {
-        pass_regs_T<MA>(xs, k, twT);
+        pass_regs_T<R, MA>(xs, k, twT);
         continue;
       }
     }
@@ -416,13 +425,13 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
     constexpr int RL = G::NPASS == 2 ? G::RA : G::RB;   // last pass span
     constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row, z, l, a.tw, key);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row, z, l, a.tw, key, a.twTA);
     } else {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, false>(row, z, l, a.tw, key, a.twT16);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, false>(row, z, l, a.tw, key, a.twTA);
       block_sync<WL>();
       write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
       block_sync<WL>();
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true>(row, z, l, a.tw, key, a.twT256);
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true>(row, z, l, a.tw, key, a.twTB);
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)

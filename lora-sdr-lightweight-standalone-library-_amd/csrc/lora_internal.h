@@ -30,13 +30,28 @@ struct KArgs {
   int est_only;  // lora_estimate_offsets_batch: all symbols, raw samples, outputs only
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), 0 in production
   int fast_rot;  // LORA_PRECISION_FAST: hardware sin/cos rotation in the symbol demod
-  const cf* twT16;   // SF12: slot-major twiddles of the MA = 16 / 256 LDS passes (or null)
-  const cf* twT256;
+  const cf* twTA;  // fast kernels: slot-major twiddles of LDS pass A / B (or null)
+  const cf* twTB;
 };
 
-// Twiddle index of slot j (0..14) of a radix-16 LDS pass with butterfly group k < MA, in
-// pass_regs' order: slots 0-2 the first radix-4 stage (tw[q*k*fs1], q = 1..3, fs1 =
-// N/(4*MA)), slots 3+3*uu+(q-1) the second (kk = k + MA*uu, tw[q*kk*fs2], fs2 = fs1/4).
+// Shape of the fast kernels' LDS passes for SF >= 6 (lora_demod_fast.hip Geo<SF>): pass-1
+// span R1 (8 for odd SF, radix-2 innermost; 16 for even), then pass A of span RA over
+// groups k < MA_A = R1 and pass B of span RB over k < MA_B = R1*RA (span 1 = no pass).
+struct PassShape {
+  int RA, MA_A, RB, MA_B;
+};
+__host__ __device__ constexpr PassShape pass_shape(int sf) {
+  const int R1 = (sf & 1) ? 8 : 16;
+  const int X = (1 << sf) / R1;
+  const int RA = X >= 16 ? 16 : X;
+  const int RB = X > 16 ? X / 16 : 1;
+  return PassShape{RA, R1, RB, R1 * RA};
+}
+
+// Twiddle index of slot j of a radix-16 (15 slots) or radix-4 (3 slots) LDS pass with
+// butterfly group k < MA, in pass_regs' order: slots 0-2 the first radix-4 stage
+// (tw[q*k*fs1], q = 1..3, fs1 = N/(4*MA)), slots 3+3*uu+(q-1) the second (kk = k + MA*uu,
+// tw[q*kk*fs2], fs2 = fs1/4).
 __host__ __device__ constexpr int twT_index(int N, int MA, int j, int k) {
   return j < 3 ? (j + 1) * k * (N / (4 * MA))
                : ((j - 3) % 3 + 1) * (k + MA * ((j - 3) / 3)) * (N / (16 * MA));
