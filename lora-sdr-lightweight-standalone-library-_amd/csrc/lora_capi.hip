@@ -736,10 +736,8 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   // gather.  Copies of the same table values: results unchanged (lora::twT_index).
   std::vector<std::complex<float>> twT;
   int twTA_off = -1, twTB_off = -1;
-  static const bool twt_ok = [] {
-    const char* e = std::getenv("LORA_MI355X_TWT");
-    return !(e && e[0] == '0');
-  }();
+  const char* twt_env = std::getenv("LORA_MI355X_TWT");  // A/B knob, read per plan
+  const bool twt_ok = !(twt_env && twt_env[0] == '0');
   if (twt_ok && p.sf >= 6) {
     lora::PassShape ps = lora::pass_shape((int)p.sf);
     auto add = [&](int R, int MA) {

@@ -85,18 +85,23 @@ CASES = [  # (sf, osr, hann, dechirp, F, symbols-per-frame, extra samples, kind)
 
 
 def make_plan(amd, path, *args, **kw):
-    """path "fast": register-blocked kernel; "generic": LDS reference kernel (A/B)."""
+    """path "fast": register-blocked kernels (LDS passes read slot-major twiddle copies);
+    "gather": the same kernels gathering twiddles from the natural table
+    (LORA_MI355X_TWT=0); "generic": LDS reference kernel (A/B)."""
     import os
 
     if path == "generic":
         os.environ["LORA_MI355X_GENERIC"] = "1"
+    if path == "gather":
+        os.environ["LORA_MI355X_TWT"] = "0"
     try:
         return amd.DemodPlan(*args, **kw)
     finally:
         os.environ.pop("LORA_MI355X_GENERIC", None)
+        os.environ.pop("LORA_MI355X_TWT", None)
 
 
-@pytest.mark.parametrize("path", ["fast", "generic"])
+@pytest.mark.parametrize("path", ["fast", "gather", "generic"])
 @pytest.mark.parametrize("case", CASES, ids=[f"sf{c[0]}-osr{c[1]}-h{int(c[2])}-d{int(c[3])}-{c[7]}-S{c[5]}"
                                              for c in CASES])
 def test_legacy_demod_matches_oracle(O, amd, case, path):
