@@ -446,6 +446,46 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
   return key;
 }
 
+// Two independent transforms of the same shape (the estimate's symbols 0 and 1) in
+// lockstep, for the wave-local two-pass geometries: the same operations as two
+// fft_key calls, interleaved so each transform's latency hides behind the other's.
+template <int SF, bool KEEP>
+__device__ __forceinline__ void fft_key2(cf* z0, cf* z1, cf* row0, cf* row1, int l, const KArgs& a,
+                                         uint64_t& k0, uint64_t& k1) {
+  using G = Geo<SF>;
+  static_assert(G::NPASS == 2 && G::WAVE_LOCAL, "wave-local two-pass transforms only");
+  constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
+#pragma unroll
+  for (int h = 0; h < G::G1; ++h) {
+    pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP>(z0 + h * R1, 0, a.tw);
+    pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP>(z1 + h * R1, 0, a.tw);
+  }
+  int c[G::G1];
+#pragma unroll
+  for (int h = 0; h < G::G1; ++h) c[h] = (int)(a.rev[l + T * h] >> G::LOGR1);
+#pragma unroll
+  for (int h = 0; h < G::G1; ++h)
+#pragma unroll
+    for (int u = 0; u < R1; ++u) {
+      row0[lds_slot<SF>(c[h] * R1) + u] = z0[h * R1 + u];
+      row1[lds_slot<SF>(c[h] * R1) + u] = z1[h * R1 + u];
+    }
+  wave_sync();
+  pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row0, z0, l, a.tw, k0, a.twTA);
+  pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row1, z1, l, a.tw, k1, a.twTA);
+  if constexpr (KEEP) {
+    wave_sync();
+#pragma unroll
+    for (int gg = 0; gg < P / G::RA; ++gg)
+#pragma unroll
+      for (int u = 0; u < G::RA; ++u) {
+        row0[lds_slot<SF>(l + T * gg) + lds_slot<SF>(G::MA_A * u)] = z0[gg * G::RA + u];
+        row1[lds_slot<SF>(l + T * gg) + lds_slot<SF>(G::MA_A * u)] = z1[gg * G::RA + u];
+      }
+    wave_sync();
+  }
+}
+
 // Argmax key over the T lanes of a symbol; every lane of the symbol gets the result.
 template <int SF>
 __device__ __forceinline__ uint64_t symbol_key(uint64_t key, int tid, uint64_t* red) {
@@ -534,6 +574,19 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
 // exactly as k_demod_fast does for the data symbols, giving the sync word.
 // Latency-bound (a few sequential transforms per frame): occupancy matters more than
 // ILP, so the register budget is capped at two waves per SIMD.
+#ifndef LORA_EST_PAIR
+#define LORA_EST_PAIR 1
+#endif
+template <int SF>
+struct EstGeo {
+  static constexpr int T = Geo<SF>::T;
+  static constexpr int BLOCK = T >= 64 ? 256 : 64;  // threads per block
+  static constexpr int SPB = BLOCK / T;             // frames per block
+  // symbols 0 and 1 transformed in lockstep (two LDS rows per frame)
+  // (SF 7-8; SF 6 would spill)
+  static constexpr bool PAIR = LORA_EST_PAIR && SF >= 7 && Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2;
+};
+
 template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
@@ -565,7 +618,64 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   bool have_prev = false;
   unsigned sum_t = 0;
   cf in[P], z[P];
-  for (int s = 0; s < 2; ++s) {
+  constexpr bool PAIR = EstGeo<SF>::PAIR && MODE <= 1;  // MODE 2 (osr / window) would spill
+  if constexpr (PAIR) {
+    // symbols 0 and 1 in lockstep (fft_key2); the per-symbol bookkeeping below is the
+    // same, applied in the same order (symbol 0 first)
+    cf* row1 = row + (size_t)EstGeo<SF>::SPB * rowc;
+    cf in1[P], z1[P];
+    float bp[2] = {-1e30f, -1e30f}, bfi[2] = {0.0f, 0.0f};
+    uint32_t bidx[2] = {0, 0};
+    unsigned bt[2] = {0, 0};
+    cf bbin[2] = {cf{0.0f, 0.0f}, cf{0.0f, 0.0f}};
+    for (int t = 0; t < osr; ++t) {
+      gather_points<SF, 0>(a, x + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in);
+      gather_points<SF, 0>(a, x + (int64_t)step + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in1);
+      rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
+      rotate_place<SF, false, 0>(in1, z1, 0.0f, 0.0f, hann, a.win, l);
+      uint64_t key[2];
+      fft_key2<SF, true>(z, z1, row, row1, l, a, key[0], key[1]);
+      key[0] = group_max(key[0], T);
+      key[1] = group_max(key[1], T);
+      if (l == 0) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const cf* rw = s ? row1 : row;
+          const uint32_t idx = key_index(key[s]);
+          const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
+          const cf L = rw[lds_slot<SF>((int)im1)], R = rw[lds_slot<SF>((int)ip1)],
+                   B = rw[lds_slot<SF>((int)idx)];
+          float pw, fi;
+          detect_tail(key_value(key[s]), L, R, a.power_scale, &pw, &fi);
+          if (pw > bp[s] || (legacy && pw == bp[s] && idx < bidx[s])) {
+            bp[s] = pw;
+            bidx[s] = idx;
+            bfi[s] = fi;
+            bt[s] = (unsigned)t;
+            bbin[s] = B;
+          }
+        }
+      }
+      wave_sync();  // the rows are rewritten by the next phase
+    }
+    if (l == 0) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sum_t += bt[s];
+        sum_index += (float)bidx[s] + bfi[s];
+        const float phase = lm_atan2f(bbin[s].im, bbin[s].re);
+        if (have_prev) {
+          float d = phase - prev_phase;
+          while (d > PI_F) d -= 2.0f * PI_F;
+          while (d < -PI_F) d += 2.0f * PI_F;
+          phase_diff += d;
+        }
+        prev_phase = phase;
+        have_prev = true;
+      }
+    }
+  }
+  for (int s = 0; s < (PAIR ? 0 : 2); ++s) {
     float best_p = -1e30f, best_fi = 0.0f;
     uint32_t best_idx = 0;
     unsigned best_t = 0;
@@ -646,7 +756,26 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   block_sync<G::WAVE_LOCAL>();
   const FrameParams q = sp[g];
   uint32_t sw[2];
-  for (int s = 0; s < 2; ++s) {
+  if constexpr (PAIR) {
+    cf* row1 = row + (size_t)EstGeo<SF>::SPB * rowc;
+    cf in1[P], z1[P];
+    int64_t base0, base1;
+    int cg0, cg1;
+    sym_base(0, step, a.frame_len, q.t_off, base0, cg0);
+    sym_base(1, step, a.frame_len, q.t_off, base1, cg1);
+    const float st0 = q.rate * ((float)((uint32_t)0 * (uint32_t)N) + (float)q.t_off / (float)osr);
+    const float st1 = q.rate * ((float)((uint32_t)1 * (uint32_t)N) + (float)q.t_off / (float)osr);
+    const float sc = (legacy && q.scaled) ? q.scale : 1.0f;
+    gather_points<SF, 0>(a, x + base0, l, osr, step, cg0, legacy ? 1 : 2, dech, sc, in);
+    gather_points<SF, 0>(a, x + base1, l, osr, step, cg1, legacy ? 1 : 2, dech, sc, in1);
+    rotate_place<SF, true, 0>(in, z, st0, q.rate, hann, a.win, l);
+    rotate_place<SF, true, 0>(in1, z1, st1, q.rate, hann, a.win, l);
+    uint64_t k0, k1;
+    fft_key2<SF, false>(z, z1, row, row1, l, a, k0, k1);
+    sw[0] = key_index(group_max(k0, T));
+    sw[1] = key_index(group_max(k1, T));
+  }
+  for (int s = 0; s < (PAIR ? 0 : 2); ++s) {
     int64_t base;
     int cg;
     sym_base(s, step, a.frame_len, q.t_off, base, cg);
@@ -677,7 +806,7 @@ bool launch_est_mode(const KArgs& a, int64_t frames, hipStream_t st) {
   constexpr int BLOCK = T >= 64 ? 256 : 64;
   constexpr int SPB = BLOCK / T;
   const int rowc = row_complex<SF>();
-  const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * (size_t)SPB * rowc;
+  const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * (size_t)SPB * rowc * (EstGeo<SF>::PAIR && MODE <= 1 ? 2 : 1);
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
     if (hipFuncSetAttribute((const void*)k_est_fast<SF, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
