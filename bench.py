@@ -7,10 +7,16 @@ CFO rotation, FFT, argmax, sync word.  Inputs are generated on the device by the
 bit-exact GPU modulator (lora_mod_batch), random symbols from a fixed seed.
 
 Headline workload (BASELINE.json configs[1]): SF7 BW125 osr 1, 1,000,000 data symbols
-= 15,625 frames x (2 sync + 64 data) per GPU.  The SF12 configuration (configs[2]) is
-measured in the same run and reported under "extra".  Multi-GPU: one process per GPU,
-frames sharded (no collective on the data path), weak scaling; value = data symbols of
-all ranks / max-over-ranks time.
+= 15,625 frames x (2 sync + 64 data) per GPU.  The SF12 configuration (configs[2]) and
+configs[4] (8 channels x 1e6 SF7 frames of 16 data symbols, one channel per GPU) are
+measured in the same run and reported under "extra", with the data-dependent slow
+rotation path (sync 0xFF), an AWGN 0 dB batch, the modulator and the CPU baselines.
+
+Multi-GPU: one process per GPU, frames sharded, no collective on the data path (weak
+scaling; value = data symbols of all ranks / max-over-ranks time).  `--gpus N` starts
+the N rank processes itself when not launched by torchrun (the parent never touches the
+GPU); ranks meet over gloo (host TCP) for the timing barrier and the max/sum of the
+timings only - RCCL is not used at all.
 
 Prints ONE JSON line on rank 0.
 """
@@ -18,59 +24,121 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "lora-sdr-lightweight-standalone-library-_amd"))
 sys.path.insert(0, REPO)
 
-import lora_phy_amd as amd  # noqa: E402
-from lora_phy_amd import _capi  # noqa: E402
-from lora_phy_amd.shard import aggregate_throughput  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 METRIC = "Msymbols/s dechirp+FFT+argmax @ SF7 & SF12, 1/2/4/8 GPU; % HBM roofline"
+SYNC = 0x12
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_setup(n_gpus):
-    """One process per GPU (torchrun).  The collectives are only the timing barrier and
-    the max/sum all-reduces (lora_phy_amd.shard); frames never cross GPUs.  Backend
-    "nccl" (RCCL) by default; LORA_BENCH_BACKEND=gloo rehearses the multi-rank path with
-    several ranks on fewer GPUs (ranks share devices round-robin)."""
+# ---------------------------------------------------------------------------------
+# Rank formation (no torchrun needed, no RCCL)
+# ---------------------------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(argv, n):
+    """Start `n` copies of this script as ranks 0..n-1 (children, not exec: this parent
+    has not initialised the GPU and never does).  Rank 0's stdout is ours; the others'
+    stdout goes to stderr.  Returns the worst exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                    "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                    "LORA_BENCH_SPAWNED": "1"})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def dist_setup(n_gpus, plumbing=False):
+    """Join the job: WORLD_SIZE from the environment (torchrun or spawn_ranks); it must
+    equal --gpus.  Rank r uses device LOCAL_RANK.  gloo (host TCP) carries the barrier
+    and the max/sum all-reduces of the timings - no RCCL."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}; run `python bench.py "
+                         f"--gpus N` (it starts the N ranks itself) or torchrun --nproc-per-node N")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not plumbing:
+        import torch
+
+        ndev = torch.cuda.device_count()
+        if local >= ndev:
+            raise SystemExit(f"bench.py: rank needs device {local} but {ndev} are visible")
+        torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
 
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        backend = os.environ.get("LORA_BENCH_BACKEND", "nccl")
-        dev = local % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(dev)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(backend)
-        return dist, dist.get_rank(), world
-    torch.cuda.set_device(0)
-    return None, 0, 1
+        dist.init_process_group("gloo")
+        return dist, dist.get_rank(), world, local
+    return None, 0, 1, local
 
 
-SYNC = 0x12
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
 
 
-def make_input(sf, frames, data_syms, seed, device, snr_db=None):
+def all_max_sum(dist, seconds, units):
+    """(max seconds, sum units) over ranks (gloo, host tensors)."""
+    if dist is None:
+        return seconds, units
+    import torch
+
+    t = torch.tensor([seconds], dtype=torch.float64)
+    u = torch.tensor([units], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(u, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(u.item())
+
+
+def gather_obj(dist, obj, world):
+    if dist is None:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+# ---------------------------------------------------------------------------------
+# Workloads
+# ---------------------------------------------------------------------------------
+
+def make_input(sf, frames, data_syms, seed, device, snr_db=None, sync=None):
+    import numpy as np
+    import torch
+
+    import lora_phy_amd as amd
+
     g = torch.Generator(device="cpu").manual_seed(seed)
     syms = torch.randint(0, 1 << sf, (frames, data_syms), generator=g, dtype=torch.int32)
-    iq = amd.modulate(syms.to(device), sf, 1, 125000, 1.0, SYNC)
+    iq = amd.modulate(syms.to(device), sf, 1, 125000, 1.0, SYNC if sync is None else sync)
     if snr_db is not None:
+        # awgn_sweep_gtest.cpp:76-80: sigma = 10^(-SNR/20), sigma/sqrt(2) per component
         sigma = 10.0 ** (-snr_db / 20.0) / np.sqrt(2.0)
         gn = torch.Generator(device=device).manual_seed(seed + 1)
         noise = torch.randn(iq.shape + (2,), generator=gn, device=device) * sigma
@@ -78,30 +146,14 @@ def make_input(sf, frames, data_syms, seed, device, snr_db=None):
     return syms, iq
 
 
-def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=None, precision="exact",
-               inputs=None):
-    N = 1 << sf
-    syms, iq = inputs if inputs is not None else make_input(sf, frames, data_syms, 20251015 + rank, device,
-                                                            snr_db)
-    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device,
-                         precision=precision)
-    out = None
-    for _ in range(warmup):
-        out = plan.run(iq, out)
-    torch.cuda.synchronize(device)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        out = plan.run(iq, out)
-    torch.cuda.synchronize(device)
-    if dist is not None:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    # Per-kernel durations: a second pass of the same steps with HIP events around every
-    # launch, recorded on the stream each kernel runs on (not inside the timed region).
+def stage_times(plan, iq, out, steps, device):
+    """Per-kernel durations: a second pass of the same steps with HIP events around every
+    launch, recorded on the stream each kernel runs on (outside the timed region)."""
     import ctypes as C
+
+    import torch
+
+    from lora_phy_amd import _capi
 
     lib = _capi.lib()
     _capi.check(lib.lora_demod_profile_enable(plan._h, steps))
@@ -112,47 +164,85 @@ def run_config(sf, frames, data_syms, steps, warmup, rank, dist, device, snr_db=
     calls = C.c_int()
     _capi.check(lib.lora_demod_profile_read(plan._h, stage, C.byref(calls)))
     lib.lora_demod_profile_enable(plan._h, 0)
-    stage_ms = [stage[k] / max(calls.value, 1) for k in range(3)]
-    # weak scaling: every rank owns its frames; units summed, time = max over ranks
-    units, wall, _ = aggregate_throughput(frames * data_syms * steps, wall)
-    ok = bool(torch.equal(out.symbols.to(torch.int32).cpu(), syms)) if snr_db is None else None
+    return [stage[k] / max(calls.value, 1) for k in range(3)], out
+
+
+def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, precision="exact",
+               inputs=None, sync=None, seed_base=20251015, rank=0):
+    import torch
+
+    import lora_phy_amd as amd
+
+    N = 1 << sf
+    syms, iq = inputs if inputs is not None else make_input(sf, frames, data_syms, seed_base + rank, device,
+                                                            snr_db, sync)
+    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device,
+                         precision=precision)
+    out = None
+    for _ in range(warmup):
+        out = plan.run(iq, out)
+    torch.cuda.synchronize(device)
+    barrier(dist)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = plan.run(iq, out)
+    torch.cuda.synchronize(device)
+    barrier(dist)
+    wall = time.perf_counter() - t0
+    stage_ms, out = stage_times(plan, iq, out, steps, device)
+    wall_max, units = all_max_sum(dist, wall, frames * data_syms * steps)
     total_syms = data_syms + 2
     ms_step = wall * 1e3 / steps
     B_sym = 8 * N + 2
-    # Dominant kernel = stage 2 (k_demod: every non-sync symbol).  Algorithmic bytes
-    # per launch = its symbols x (8*N*osr IQ read + 2 B index write).
-    demod_bytes = frames * data_syms * B_sym
-    dom_gbs = demod_bytes / (stage_ms[2] * 1e-3) / 1e9
-    pipe_bytes = frames * (total_syms * B_sym + 9)
+    got = out.symbols.to(torch.int32).cpu()
+    ser = float((got != syms).float().mean())
+    dom = max(range(3), key=lambda k: stage_ms[k])
+    # algorithmic bytes: every symbol's IQ read once + its u16 index
+    # write, plus 9 B of per-frame outputs
+    step_bytes = frames * (total_syms * B_sym + 9)
+    # the dominant kernel's own algorithmic bytes per launch
+    dom_bytes = {0: frames * total_syms * 8 * N,             # frame max: the whole IQ
+                 1: frames * (2 * 8 * N + 9),                 # estimate: symbols 0/1 + outputs
+                 2: frames * data_syms * B_sym}[dom]          # demod: data symbols
+    dom_gbs = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9
     return {
         "sf": sf, "frames": frames, "data_symbols": frames * data_syms, "iq_bytes": iq.numel() * 8,
-        "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ok,
+        "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ser == 0.0, "ser_vs_tx": ser,
         "msym_s_data": frames * data_syms / (ms_step * 1e-3) / 1e6,
-        "msym_s_all_ranks": units / wall / 1e6,
+        "msym_s_all_ranks": units / wall_max / 1e6, "ms_per_step_max_rank": wall_max * 1e3 / steps,
         "msym_s_all": frames * total_syms / (ms_step * 1e-3) / 1e6,
-        "dominant_kernel": "k_demod", "dominant_gbs": dom_gbs,
-        "dominant_bytes_per_launch": demod_bytes,
-        "pipeline_gbs": pipe_bytes / (ms_step * 1e-3) / 1e9,
-        "iq_host": None, "plan": plan, "iq": iq, "syms": syms,
+        "dominant_kernel": ["k_frame_max", "k_est_fast", "k_demod_fast"][dom], "dominant_stage": dom,
+        "dominant_gbs": dom_gbs, "dominant_bytes_per_launch": dom_bytes,
+        "step_bytes": step_bytes, "pipeline_gbs": step_bytes / (ms_step * 1e-3) / 1e9,
+        "plan": plan, "iq": iq, "syms": syms, "out": out,
     }
 
 
-def run_channels(frames, data_syms, steps, warmup, rank, dist, device, chunk_bytes=8e9):
+def public(r):
+    return {k: v for k, v in r.items() if k not in ("plan", "iq", "syms", "out")}
+
+
+def run_channels(frames, data_syms, steps, warmup, dist, device, rank, chunk_bytes=8e9):
     """BASELINE.json configs[4]: one channel per GPU, `frames` SF7 frames of 2 + `data_syms`
     symbols resident in HBM (18.4 GB at 1e6 x 16), demodulated in <= 8 GB chunks per step
-    (SURVEY.md 8d item 5).  Inputs generated on the device (GPU modulator) in slices."""
+    (SURVEY.md 8d item 5).  Inputs generated on the device (GPU modulator) in slices;
+    every frame's symbols are checked against the transmitted ones (noiseless)."""
+    import torch
+
+    import lora_phy_amd as amd
+
     sf, N = 7, 128
     L = (data_syms + 2) * N
     iq = torch.empty((frames, L), dtype=torch.complex64, device=device)
+    tx = torch.empty((frames, data_syms), dtype=torch.int16, device=device)
     g = torch.Generator(device="cpu").manual_seed(4242 + rank)
     gen_rows = 1 << 17
-    first_syms = None
     for r0 in range(0, frames, gen_rows):
         n = min(gen_rows, frames - r0)
-        syms = torch.randint(0, N, (n, data_syms), generator=g, dtype=torch.int32)
-        if first_syms is None:
-            first_syms = syms[:64].clone()
-        iq[r0:r0 + n] = amd.modulate(syms.to(device), sf, 1, 125000, 1.0, SYNC)
+        syms = torch.randint(0, N, (n, data_syms), generator=g, dtype=torch.int32).to(device)
+        tx[r0:r0 + n] = syms.to(torch.int16)
+        iq[r0:r0 + n] = amd.modulate(syms, sf, 1, 125000, 1.0, SYNC)
     plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device)
     per_chunk = max(1, int(chunk_bytes // (L * 8)))
     chunks = [(c0, min(per_chunk, frames - c0)) for c0 in range(0, frames, per_chunk)]
@@ -165,21 +255,51 @@ def run_channels(frames, data_syms, steps, warmup, rank, dist, device, chunk_byt
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(device)
-    if dist is not None:
-        dist.barrier()
+    barrier(dist)
+    torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize(device)
-    if dist is not None:
-        dist.barrier()
+    barrier(dist)
     wall = time.perf_counter() - t0
-    units, wall_max, _ = aggregate_throughput(frames * data_syms * steps, wall)
-    ok = bool(torch.equal(outs[0].symbols[:64].to(torch.int32).cpu(), first_syms))
-    del iq
+    wall_max, units = all_max_sum(dist, wall, frames * data_syms * steps)
+    bad = 0
+    for (c0, n), o in zip(chunks, outs):
+        bad += int((o.symbols.to(torch.int16) != tx[c0:c0 + n]).sum())
+    del iq, tx
     return {"frames_per_gpu": frames, "data_symbols_per_frame": data_syms, "iq_gb_per_gpu": frames * L * 8 / 1e9,
-            "chunks": len(chunks), "ms_per_step": wall_max * 1e3 / steps,
-            "value_all_ranks_msym_s": units / wall_max / 1e6, "symbols_ok_first64": ok}
+            "chunks": len(chunks), "ms_per_step": wall * 1e3 / steps,
+            "ms_per_step_max_rank": wall_max * 1e3 / steps,
+            "value_all_ranks_msym_s": units / wall_max / 1e6,
+            "symbols_ok_all_frames": bad == 0, "symbol_mismatches": bad}
+
+
+def run_modulator(sf, frames, data_syms, device, reps=3):
+    """lora_mod_batch throughput: samples written per second and the
+    HBM write rate (8 B per sample written, symbol reads negligible)."""
+    import torch
+
+    import lora_phy_amd as amd
+
+    g = torch.Generator(device="cpu").manual_seed(99)
+    syms = torch.randint(0, 1 << sf, (frames, data_syms), generator=g, dtype=torch.int32).to(device)
+    syms16 = syms.to(torch.uint16)
+    out = amd.modulate(syms16, sf)
+    torch.cuda.synchronize(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        out = amd.modulate(syms16, sf)
+    e1.record()
+    torch.cuda.synchronize(device)
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = out.numel() * 8
+    del out
+    torch.cuda.empty_cache()
+    return {"sf": sf, "frames": frames, "symbols_per_frame": data_syms + 2, "ms_per_call": ms,
+            "msym_s": frames * (data_syms + 2) / (ms * 1e-3) / 1e6, "write_gbs": nbytes / (ms * 1e-3) / 1e9,
+            "roofline_frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_written": nbytes}
 
 
 def _cpu_model():
@@ -192,25 +312,41 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=10.0):
+def host_cores():
+    """CPUs this process may run on: sched_getaffinity, capped by a cgroup CPU quota
+    (cpu.max) when one is set - threads beyond the quota only time-slice."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    used = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return {"sched_getaffinity": aff, "cgroup_quota_cpus": quota, "used": used}
+
+
+def cpu_baseline(sf, iq_dev, data_syms, max_frames, time_budget_s=10.0):
     """The reference's own lora_demodulate (oracle/_ref, compiled from the reference's
-    sources, travels with the snapshot) on `threads` host cores over a bounded sample of
-    the same frames; falls back to the restatement (oracle/lora_oracle.cpp) if absent.
-    Reported `value`: all threads, caller-side dechirp + lora_demodulate (the GPU
-    workload).  Also: one core, and demod only (input dechirped beforehand), per
-    SURVEY.md 8d.  The reported leg: whole passes over the sample until `time_budget_s`
-    (about 10 s of CPU work); the single-core and demod-only legs: half that."""
+    sources, travels with the snapshot) on every usable host core (host_cores) over a
+    bounded sample of the same frames; the restatement (oracle/lora_oracle.cpp) if the
+    reference build is absent.  Reported `value`: all threads, caller-side dechirp +
+    lora_demodulate (the GPU workload).  Also: one core, and demod only (input dechirped
+    beforehand), per SURVEY.md 8d."""
     from oracle.pyoracle import Oracle, Reference
 
     if Reference.available():
         impl, kind, what = Reference(), "reference", "reference src/phy lora_demodulate (oracle/_ref)"
     else:
         impl, kind, what = Oracle(), "port", "restatement oracle/lora_oracle.cpp"
+    cores = host_cores()
+    threads = cores["used"]
     F = min(iq_dev.shape[0], max_frames)
     x = iq_dev[:F].cpu().numpy()
 
     def rate(xs, nthreads, dechirp, budget):
-        impl.demod_frames(xs[: min(len(xs), 4 * nthreads)], sf, 1, False, dechirp=dechirp, threads=nthreads)
+        impl.demod_frames(xs[: min(len(xs), nthreads)], sf, 1, False, dechirp=dechirp, threads=nthreads)
         t0 = time.perf_counter()
         done = 0
         while True:
@@ -222,14 +358,15 @@ def cpu_baseline(sf, iq_dev, data_syms, max_frames, threads, time_budget_s=10.0)
         return done * data_syms / dt / 1e6, done, dt
 
     all_rate, done, dt = rate(x, threads, True, time_budget_s)
-    one_rate, _, _ = rate(x[: max(1, F // max(threads, 1))], 1, True, time_budget_s / 2)
+    one_rate, _, _ = rate(x[: max(1, min(F, 4))], 1, True, time_budget_s / 3)
     xd = Oracle().dechirp(x.reshape(-1), sf).reshape(x.shape)  # same fp32 products as the caller loop
-    demod_only, _, _ = rate(xd, threads, False, time_budget_s / 2)
+    demod_only, _, _ = rate(xd, threads, False, time_budget_s / 3)
     return {"value": all_rate, "unit": "Msymbols/s", "cores": threads, "kind": kind,
-            "single_core": one_rate, "demod_only_all_cores": demod_only, "cpu_model": _cpu_model(),
-            "sample": f"{done} frames of the SF{sf} bench batch ({data_syms}+2 symbols each), "
-                      f"caller-side dechirp + {what}, {threads} threads, {dt:.2f} s; single_core: same "
-                      f"on 1 thread; demod_only: input dechirped beforehand"}
+            "host_cores": cores, "single_core": one_rate, "demod_only_all_cores": demod_only,
+            "cpu_model": _cpu_model(),
+            "sample": f"{done} frames of the SF{sf} bench batch ({data_syms}+2 symbols each, {F} distinct), "
+                      f"caller-side dechirp + {what}, {threads} threads, {dt:.2f} s; single_core: same on 1 "
+                      f"thread; demod_only: input dechirped beforehand"}
 
 
 def fast_summary(r):
@@ -237,13 +374,22 @@ def fast_summary(r):
     include/lora_mi355x.h): same workload and inputs as the exact run."""
     return {"precision": "fast", "ms_per_step": r["ms_per_step"], "stage_ms": r["stage_ms"],
             "symbols_ok": r["symbols_ok"], "value_all_ranks_msym_s": r["msym_s_all_ranks"],
-            "demod_gbs": r["dominant_gbs"], "demod_roofline_frac": r["dominant_gbs"] / HBM_PEAK_GBS}
+            "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS}
+
+
+def variant_summary(r, base, note):
+    return {"note": note, "ms_per_step": r["ms_per_step"], "stage_ms": r["stage_ms"],
+            "value_all_ranks_msym_s": r["msym_s_all_ranks"], "ser_vs_tx": r["ser_vs_tx"],
+            "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS,
+            "ratio_to_headline": r["ms_per_step"] / base["ms_per_step"]}
 
 
 def hbm_probe(device, nbytes=2 << 30, reps=5):
     """SURVEY.md 8d cross-check: device-to-device copy bandwidth on the same GPU
     (bytes read + bytes written per second), the chip's achievable HBM rate next to the
     8 TB/s spec."""
+    import torch
+
     src = torch.empty(nbytes, dtype=torch.uint8, device=device)
     dst = torch.empty_like(src)
     dst.copy_(src)
@@ -272,22 +418,26 @@ def load_pmc(workload, key="hbm_bytes_per_launch"):
         return None
 
 
-def valu_roofline(workload, kernel_ms):
-    """The demod kernel's real limit: VALU issue.  Counts from the committed PMC profile
-    (profiles/pmc_summary.json, same kernel and workload) against the live kernel time;
-    peak = the time the profiled fp32/fp64 instruction mix needs at the chip's measured
-    issue rates (tools/micro/pk_rate)."""
-    v = load_pmc(workload, "valu_winstr_per_launch")
-    need = load_pmc(workload, "valu_mix_ns_cu")
-    if not v or not need or not kernel_ms:
-        return None
-    ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    achieved = v / (kernel_ms * 1e6) / ncu  # wave-instructions per ns per CU
-    return {"bound": "valu-issue", "winstr_per_launch": v,
-            "fp64_class_per_launch": load_pmc(workload, "valu_fp64_class_per_launch"),
-            "achieved_winstr_per_ns_per_cu": achieved,
-            "frac": need / ncu / (kernel_ms * 1e6),
-            "note": "frac = (profiled instruction mix at measured peak issue rates) / live kernel time"}
+def roofline(r, probe=None):
+    """roofline object for one workload: the dominant kernel (HIP-event time, algorithmic
+    bytes per launch) and the whole step (pipeline_frac); counter bytes from the
+    committed rocprofv3 profile (profiles/pmc_summary.json, labelled as such)."""
+    wl = "sf%d" % r["sf"]
+    pmc_step = load_pmc(wl, "hbm_bytes_per_step")
+    pmc_dom = load_pmc(wl, "hbm_bytes_per_launch")
+    return {"bound": "hbm", "kernel": r["dominant_kernel"],
+            "achieved": r["dominant_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": r["dominant_gbs"] / HBM_PEAK_GBS,
+            "bytes_per_launch": r["dominant_bytes_per_launch"],
+            "traffic": pmc_dom,
+            "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, committed; "
+                              "not measured in this run)",
+            "pipeline": {"algorithmic_bytes_per_step": r["step_bytes"], "ms_per_step": r["ms_per_step"],
+                         "achieved": r["pipeline_gbs"], "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS,
+                         "counter_bytes_per_step": pmc_step,
+                         "counter_over_algorithmic": (pmc_step / r["step_bytes"]) if pmc_step else None},
+            "hbm_probe": {"d2d_copy_gbs": probe,
+                          "note": "achievable rate on this GPU: torch D2D copy (read+write)"}}
 
 
 def main():
@@ -303,49 +453,84 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-channels", action="store_true", help="skip the configs[4] measurement")
     ap.add_argument("--no-fast", action="store_true", help="skip the LORA_PRECISION_FAST lines")
+    ap.add_argument("--no-variants", action="store_true", help="skip the sync-0xFF / AWGN / modulator lines")
     ap.add_argument("--channel-frames", type=int, default=1_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--sync", type=lambda v: int(v, 0), default=0x12,
-                    help="sync word of the synthetic frames (0x12 = the reference default; "
-                         "large nibbles -> large estimated CFO -> phases past the fast sincos range)")
+                    help="sync word of the synthetic frames (0x12 = the reference default)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="form the ranks and report them without touching a GPU (CPU test of the "
+                         "multi-rank launch)")
     args = ap.parse_args()
     global SYNC
     SYNC = args.sync
 
-    dist, rank, world = dist_setup(args.gpus)
-    device = torch.device("cuda", torch.cuda.current_device())
-    if args.sf12_only:
-        r12 = run_config(12, args.sf12_frames, args.data_symbols, args.steps, args.warmup, rank, dist,
-                         device)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
+    dist, rank, world, local = dist_setup(args.gpus, args.plumbing)
+    ranks = gather_obj(dist, {"rank": rank, "device": local, "pid": os.getpid()}, world)
+    if args.plumbing:
+        wall_max, units = all_max_sum(dist, 0.001 * (rank + 1), 1000)
         if rank == 0:
-            print(json.dumps({k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host", "syms")}))
+            print(json.dumps({"plumbing": True, "n_gpus": world, "ranks": ranks,
+                              "max_seconds": wall_max, "units": units}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
         return
-    r7 = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, rank, dist, device)
+
+    import torch
+
+    device = torch.device("cuda", local)
+    if args.sf12_only:
+        r12 = run_config(12, args.sf12_frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank)
+        if rank == 0:
+            print(json.dumps(public(r12)))
+        return
+    r7 = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank)
     extra = {}
     if not args.no_fast:
-        r7f = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, rank, dist, device,
-                         precision="fast", inputs=(r7["syms"], r7["iq"]))
+        r7f = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device,
+                         precision="fast", inputs=(r7["syms"], r7["iq"]), rank=rank)
         extra["fast_rotation_sf7"] = fast_summary(r7f)
         del r7f
+    if not args.no_variants:
+        # data-dependent slow rotation path: sync nibbles 0xF -> estimated cfo ~0.94 ->
+        # phases up to ~400 rad, past glibc sincosf's |x| < 120 fast reduction
+        rff = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, sync=0xFF,
+                         rank=rank)
+        extra["sync_ff_sf7"] = variant_summary(rff, r7, "sync 0xFF: large estimated CFO, Payne-Hanek "
+                                                        "reduction in the rotation (ser_vs_tx is the reference's "
+                                                        "own CFO-shift behaviour, not an error)")
+        del rff
+        rn = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, snr_db=0.0,
+                        rank=rank)
+        extra["awgn_0db_sf7"] = variant_summary(rn, r7, "AWGN 0 dB (sigma/sqrt2 per component, "
+                                                       "awgn_sweep_gtest.cpp:76-80); t_off != 0 frames")
+        del rn
+        torch.cuda.empty_cache()
+        extra["mod_sf7"] = run_modulator(7, args.frames, args.data_symbols, device)
+    r12 = None
     if not args.no_sf12:
         r12 = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2),
-                         args.warmup, rank, dist, device)
-        extra["sf12"] = {k: v for k, v in r12.items() if k not in ("plan", "iq", "iq_host", "syms")}
+                         args.warmup, dist, device, rank=rank)
+        extra["sf12"] = public(r12)
         extra["sf12"]["value_all_ranks_msym_s"] = r12["msym_s_all_ranks"]
-        extra["sf12"]["roofline_frac"] = r12["dominant_gbs"] / HBM_PEAK_GBS
-        extra["sf12"]["traffic"] = load_pmc("sf12")
-        extra["sf12"]["valu"] = valu_roofline("sf12", r12["stage_ms"][2])
-        extra["sf12"]["frame_max_read_gbs"] = r12["iq_bytes"] / (r12["stage_ms"][0] * 1e-3) / 1e9
+        extra["sf12"]["roofline"] = roofline(r12)
         if not args.no_fast:
-            r12f = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2), args.warmup, rank,
-                              dist, device, precision="fast", inputs=(r12["syms"], r12["iq"]))
+            r12f = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2), args.warmup,
+                              dist, device, precision="fast", inputs=(r12["syms"], r12["iq"]), rank=rank)
             extra["fast_rotation_sf12"] = fast_summary(r12f)
             del r12f
+        if rank == 0 and not args.no_cpu and world == 1:
+            try:
+                extra["sf12"]["cpu_baseline"] = cpu_baseline(12, r12["iq"], args.data_symbols, 64)
+            except Exception as e:  # the CPU leg must not kill the GPU measurement
+                log("sf12 cpu baseline failed:", e)
         del r12
         torch.cuda.empty_cache()
-    if not args.no_channels and not args.sf12_only:
-        extra["channels"] = run_channels(args.channel_frames, 16, max(args.steps // 4, 2), 1, rank, dist,
-                                         device)
+        if not args.no_variants:
+            extra["mod_sf12"] = run_modulator(12, 2000, args.data_symbols, device)
+    if not args.no_channels:
+        extra["channels"] = run_channels(args.channel_frames, 16, max(args.steps // 4, 2), 1, dist, device, rank)
         torch.cuda.empty_cache()
     probe = None
     try:
@@ -355,7 +540,7 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
         try:
-            cpu = cpu_baseline(7, r7["iq"], args.data_symbols, 4000, args.cpu_threads)
+            cpu = cpu_baseline(7, r7["iq"], args.data_symbols, 4000)
         except Exception as e:  # the CPU leg must not kill the GPU measurement
             log("cpu baseline failed:", e)
     if rank == 0:
@@ -368,7 +553,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": r7["ms_per_step"],
+            "ms_per_step": r7["ms_per_step_max_rank"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -376,20 +561,11 @@ def main():
             "data": "synthetic (GPU lora_modulate of seeded random symbols, amplitude 1, no noise)",
             "config": {"workload": workload, "sf": 7, "bw_hz": 125000, "osr": 1,
                        "frames_per_gpu": args.frames, "data_symbols_per_frame": args.data_symbols,
-                       "parallelism": f"frames sharded x{world}, no collective",
-                       "symbols_ok": r7["symbols_ok"], "stage_ms": r7["stage_ms"],
+                       "parallelism": f"frames sharded x{world}, no collective (gloo timing only)",
+                       "ranks": ranks, "symbols_ok": r7["symbols_ok"], "stage_ms": r7["stage_ms"],
                        "msym_s_all_symbols": r7["msym_s_all"] * world,
                        "pipeline_gbs_per_gpu": r7["pipeline_gbs"]},
-            "roofline": {"bound": "hbm", "kernel": r7["dominant_kernel"],
-                         "achieved": r7["dominant_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": r7["dominant_gbs"] / HBM_PEAK_GBS,
-                         "bytes_per_launch": r7["dominant_bytes_per_launch"],
-                         "traffic": load_pmc("sf7"),
-                         "valu": valu_roofline("sf7", r7["stage_ms"][2]),
-                         "hbm_probe": {"d2d_copy_gbs": probe,
-                                       "frame_max_read_gbs": r7["iq_bytes"] / (r7["stage_ms"][0] * 1e-3) / 1e9,
-                                       "note": "achievable rates on this GPU: torch D2D copy (read+write) and "
-                                               "the k_frame_max streaming read of the same IQ"}},
+            "roofline": roofline(r7, probe),
             "cpu_baseline": cpu,
             "extra": extra,
         }
