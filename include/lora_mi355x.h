@@ -166,6 +166,18 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
 int lora_demod_profile_enable(lora_demod_plan* plan, int max_calls);
 int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls);
 
+/* Which kernels the plan's last lora_demod_batch call launched (bit mask, for tests and
+ * measurement): the three-launch path is FRAME_MAX (LEGACY) + ESTIMATE + DEMOD; the
+ * frame-resident single-read kernel (LEGACY, osr 1, no window, SF 6-8, frames whose LDS
+ * image fits) is FUSED alone; GENERIC marks the LDS reference kernels.  0 before the
+ * first call.  Host-side bookkeeping only. */
+#define LORA_KERNEL_FRAME_MAX 1
+#define LORA_KERNEL_ESTIMATE 2
+#define LORA_KERNEL_DEMOD 4
+#define LORA_KERNEL_FUSED 8
+#define LORA_KERNEL_GENERIC 16
+int lora_demod_last_kernels(const lora_demod_plan* plan);
+
 /* Thread-local text of the last error ("" if none). */
 const char* lora_last_error(void);
 

@@ -640,6 +640,8 @@ struct lora_demod_plan {
   int use_fast;  // 0: generic LDS kernel only (LORA_MI355X_GENERIC=1, for A/B checks)
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), results invalid
   int max_chunks;  // 2-stream pipeline depth (LORA_MI355X_CHUNKS, default 1 = off)
+  size_t fused_lds_max;  // frame-resident single-read kernel: LDS image limit (0 = off)
+  int last_kernels = 0;  // LORA_KERNEL_* mask of the last lora_demod_batch call
   // Two-stream pipeline: per-frame prep (max + estimate) of chunk c+1 on `aux`
   // overlaps the symbol demod of chunk c on the caller's stream.
   hipStream_t aux = nullptr;
@@ -687,6 +689,8 @@ extern "C" {
 const char* lora_version(void) { return "lora_mi355x 0.1 (gfx950)"; }
 
 const char* lora_last_error(void) { return g_last_error.c_str(); }
+
+int lora_demod_last_kernels(const lora_demod_plan* plan) { return plan ? plan->last_kernels : 0; }
 
 int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** out) {
   if (!params || !out) return set_error(LORA_EINVAL, "null argument");
@@ -776,6 +780,13 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
     plan->ablate = ab ? std::atoi(ab) : 0;
     const char* ch = std::getenv("LORA_MI355X_CHUNKS");
     plan->max_chunks = std::max(1, std::min(kMaxChunks, ch ? std::atoi(ch) : 1));
+    // Frame-resident single-read kernel (k_frame_fused), opt-in: LORA_MI355X_FUSED = its LDS
+    // image limit in KiB (80 = two frames per CU), unset or 0 = off.  It is bit-exact but
+    // slower than the three launches on the measured workloads:
+    // its per-frame estimate chain is serial latency that two frames per CU cannot hide.
+    const char* fu = std::getenv("LORA_MI355X_FUSED");
+    const int fk = fu ? std::max(0, std::min(160, std::atoi(fu))) : 0;
+    plan->fused_lds_max = fk == 0 ? 0 : (size_t)fk * 1024 - (fk <= 80 ? 256 : 128);
   }
   plan->dev_tables = mem;
   plan->tw = reinterpret_cast<cf*>(b);
@@ -968,8 +979,10 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     return set_error(LORA_EINVAL, "batch too large");
   }
   // Per-frame prep of one chunk: (LEGACY) frame max, then estimate + sync symbols.
+  int kernels = 0;
   auto prep = [&](const KArgs& ac, uint32_t* mb, int64_t nf, hipStream_t s) {
     if (p.mode == LORA_MODE_LEGACY && frame_len > 0) {
+      kernels |= LORA_KERNEL_FRAME_MAX;
       ProfScope ps(plan, 0, s);
       if (max_wave)
         hipLaunchKernelGGL(k_frame_max_wave, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, s, ac, nf, mb);
@@ -977,14 +990,19 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
         hipLaunchKernelGGL(k_frame_max, dim3((unsigned)(nf * bpf)), dim3(256), 0, s, ac, bpf, chunk, mb);
     }
     ProfScope ps(plan, 1, s);
-    if (!plan->use_fast || !lora::launch_est_fast(ac, nf, s))
+    kernels |= LORA_KERNEL_ESTIMATE;
+    if (!plan->use_fast || !lora::launch_est_fast(ac, nf, s)) {
+      kernels |= LORA_KERNEL_GENERIC;
       hipLaunchKernelGGL(k_estimate, dim3((unsigned)nf), dim3(256), sizeof(cf) * plan->N, s, ac);
+    }
   };
   auto demod = [&](const KArgs& ac, int64_t nf, hipStream_t s) {
     const int64_t work = nf * per;
     if (work <= 0) return;
     ProfScope ps(plan, 2, s);
+    kernels |= LORA_KERNEL_DEMOD;
     if (!plan->use_fast || !lora::launch_demod_fast(ac, s0, work, s)) {
+      kernels |= LORA_KERNEL_GENERIC;
       const int G = std::max(1, 1024 / plan->N);
       hipLaunchKernelGGL(k_demod, dim3((unsigned)((work + G - 1) / G)), dim3(256),
                          sizeof(cf) * G * plan->N, s, ac, G, s0, work);
@@ -1014,7 +1032,13 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     if (e != hipSuccess) rc = set_error(LORA_EIO, "hipMemsetAsync failed");
     if (rc == LORA_OK) demod(a, frames, st);
   } else if (nchunks <= 1) {
-    if (rc == LORA_OK) {
+    bool fused = false;
+    if (plan->use_fast && plan->fused_lds_max > 0 && p.mode == LORA_MODE_LEGACY) {
+      ProfScope ps(plan, 2, st);
+      fused = lora::launch_fused(a, frames, plan->fused_lds_max, st);
+    }
+    if (fused) kernels |= LORA_KERNEL_FUSED;
+    if (!fused) {
       prep(a, maxbits, frames, st);
       demod(a, frames, st);
     }
@@ -1037,6 +1061,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     }
   }
   if (plan->prof_calls < plan->prof_max) ++plan->prof_calls;
+  plan->last_kernels = kernels;
   if (rc == LORA_OK) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) rc = set_error(LORA_EIO, std::string("kernel launch: ") + hipGetErrorString(e));

@@ -20,6 +20,9 @@
 #include "../../include/lora_mi355x.h"
 #include "lora_internal.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 #pragma clang fp contract(off)
 
 namespace lora {
@@ -794,6 +797,364 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   }
 }
 
+// ---- frame-resident pipeline: one HBM read per sample --------------------------------
+// LEGACY, osr 1, no window (MODE 0: fused caller dechirp, MODE 1: dechirped input), SF
+// 6-8, frames that fit LDS.  One workgroup per frame:
+//   load      the frame streams HBM -> registers once (16-byte nontemporal loads), is
+//             dechirped (e2e_chain_test.cpp:88-93), reduced to max(|I|,|Q|)
+//             (LoRaDemod.cpp:59-67) and stored to LDS as rows of ROW = lds_row<SF>()
+//             complex values per symbol (sample j at row j>>SF, column j&(N-1));
+//   estimate  one T-lane group: symbols 0 and 1 scaled (LoRaDemod.cpp:68-77), the
+//             offset estimate (:79-135) and the sync symbols (:165-168, 177-192), as
+//             k_est_fast, reading LDS instead of HBM (one scratch row after the frame);
+//   demod     rounds of BLOCK/T data symbols read from LDS with the t_off rule
+//             (:142-149), then each symbol's transposes run in place in its own row.
+//             The rows a round reads are never rows an earlier round wrote: with
+//             t_off >= 0 a window reaches into the next row, so rounds go up; with
+//             t_off < 0 into the previous row, so rounds go down.  One barrier per
+//             round separates its reads from its in-place writes.
+// Two workgroups share a CU (frame <= ~78 KB), so one frame's load overlaps the other's
+// arithmetic; the separate frame-max pass and its second read of the IQ are gone.
+template <int SF>
+__device__ __forceinline__ void lds_points(const cf* __restrict__ frame, int s, int e, int l, float scale,
+                                           cf* in) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P, ROW = lds_row<SF>(), PADC = ROW - N;
+  // point q of lane l: frame sample s*N + e + l + T*q (|e| < N), row-crossing folded in
+  const cf* b = frame + s * ROW + e + l;
+  if (__all(e == 0)) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) in[q] = cscale(b[T * q], scale);
+  } else {
+    const int p0 = e + l;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const int p = p0 + T * q;
+      const int c = p >= N ? PADC : (p < 0 ? -PADC : 0);
+      in[q] = cscale(b[T * q + c], scale);
+    }
+  }
+}
+
+#ifdef LORA_FUSED_TIMING
+// Development instrumentation (never in the product build): per workgroup and frame
+// iteration (first 16), s_memrealtime (100 MHz) stamps at the phase boundaries plus the hardware id.
+__device__ unsigned long long g_fused_dbg[2048 * 16 * 8];
+#define FSTAMP(it, k)                                                                          \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 2048 && (it) < 16)                                    \
+      g_fused_dbg[((size_t)blockIdx.x * 16 + (it)) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define FSTAMP(it, k) \
+  do {                \
+  } while (0)
+#endif
+
+// LDS bytes of the FFT tables k_frame_fused keeps next to the frame: tw (N), the pass-A
+// slot-major twiddles (15 or 3 slots x MA_A) and the leaf order (N x u16).
+template <int SF>
+struct FusedTables {
+  static constexpr int TWT = (Geo<SF>::RA == 16 ? 15 : 3) * Geo<SF>::MA_A;
+  static constexpr int BYTES = ((8 * (Geo<SF>::N + TWT) + 2 * Geo<SF>::N) + 15) & ~15;
+};
+
+// Estimate candidate of one symbol (LoRaDemod.cpp:86-110 with osr 1), handed from the
+// group that transformed it to thread 0.
+struct EstCand {
+  cf bin;
+  float fi;
+  uint32_t idx, take, pad;
+};
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not
+// for its global loads and stores (__syncthreads' fence also drains those: the output
+// stores and the IQ loads in flight would stall every barrier).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One frame of k_frame_fused.
+template <int SF, int MODE, bool FAST>
+__device__ __forceinline__ LORA_SCALAR_FP32 void fused_frame(const KArgs& a, int nrows, int64_t f,
+                                                                      unsigned char* smem, float* wmax,
+                                                                      FrameParams& sp, EstCand* ec, uint32_t* swl,
+                                                                      int it) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P, ROW = lds_row<SF>();
+  constexpr bool DECH = MODE == 0;
+  cf* frame = reinterpret_cast<cf*>(smem);
+  cf* er = frame + nrows * ROW;  // two scratch rows: the estimate / sync transforms of symbols 0, 1
+  // The FFT tables in LDS (copied while the frame streams in): the transforms' twiddle and
+  // leaf-order reads are then LDS reads, off the latency chain of the estimate and sync
+  // symbols and off the vector-memory path of the data symbols.
+  cf* ltw = er + 2 * ROW;
+  cf* ltwT = ltw + N;
+  uint16_t* lrev = reinterpret_cast<uint16_t*>(ltwT + FusedTables<SF>::TWT);
+  KArgs b = a;
+  b.tw = ltw;
+  b.twTA = a.twTA ? ltwT : nullptr;
+  b.rev = lrev;
+  const int nthr = blockDim.x;
+  const int len = (int)a.frame_len;
+  for (int i = threadIdx.x; i < N; i += nthr) {
+    ltw[i] = a.tw[i];
+    lrev[i] = a.rev[i];
+  }
+  if (a.twTA)
+    for (int i = threadIdx.x; i < FusedTables<SF>::TWT; i += nthr) ltwT[i] = a.twTA[i];
+  {
+    // Lane indices from an opaque per-frame copy of threadIdx.x: otherwise the
+    // frame-invariant lane addresses of every phase are hoisted out of this loop and
+    // kept live across it (spilled).
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int wv = tid >> 6;
+    const int g = tid / T;
+    const int l = tid % T;
+    const bool est_lane = wv < 2 && (tid & 63) < T;  // group 0 of waves 0 and 1
+    const cf* __restrict__ x = a.iq + f * a.frame_stride;
+    FSTAMP(it, 0);
+#ifdef LORA_FUSED_TIMING
+    if (threadIdx.x == 0 && blockIdx.x < 2048 && it < 16) {
+      unsigned hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      g_fused_dbg[((size_t)blockIdx.x * 16 + it) * 8 + 7] = ((unsigned long long)xcc << 32) | hw;
+    }
+#endif
+    // ---- load: HBM -> (dechirp) -> max -> LDS ----
+    float m = 0.0f;
+    {
+#ifndef LORA_FUSED_KB
+#define LORA_FUSED_KB 9
+#endif
+      constexpr int KB = LORA_FUSED_KB;
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const int p1 = len >> 1;
+      for (int pb = tid; pb < p1; pb += KB * nthr) {
+        f4v q[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const int pr = pb + k * nthr;
+          q[k] = pr < p1 ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x) + pr)
+                         : f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+        f4v w[KB];
+        if constexpr (DECH) {
+#pragma unroll
+          for (int k = 0; k < KB; ++k)  // table phase of an even sample is even: 16-B aligned
+            w[k] = *reinterpret_cast<const f4v*>(a.down + ((2 * (pb + k * nthr)) & (N - 1)));
+        }
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const int pr = pb + k * nthr;
+          cf v0{q[k][0], q[k][1]}, v1{q[k][2], q[k][3]};
+          if constexpr (DECH) {
+            v0 = cmul(v0, cf{w[k][0], w[k][1]});
+            v1 = cmul(v1, cf{w[k][2], w[k][3]});
+          }
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(v0.re), fabsf(v0.im)), fmaxf(fabsf(v1.re), fabsf(v1.im))));
+          if (pr < p1) {
+            const int j = 2 * pr;
+            *reinterpret_cast<f4v*>(frame + (j >> SF) * ROW + (j & (N - 1))) = f4v{v0.re, v0.im, v1.re, v1.im};
+          }
+        }
+      }
+      if ((len & 1) && tid == 0) {  // odd frame length: the last sample
+        const int j = len - 1;
+        cf v = x[j];
+        if constexpr (DECH) v = cmul(v, a.down[j & (N - 1)]);
+        m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+        frame[(j >> SF) * ROW + (j & (N - 1))] = v;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((tid & 63) == 0) wmax[wv] = m;
+    lds_barrier();
+    FSTAMP(it, 1);
+    float maxv = wmax[0];
+    for (int w = 1; w < (nthr >> 6); ++w) maxv = fmaxf(maxv, wmax[w]);
+    const int scaled = maxv > 1.0f;
+    const float scale = scaled ? 1.0f / maxv : 1.0f;  // LoRaDemod.cpp:68-77
+
+    // ---- offset estimate: symbol w on group 0 of wave w (w = 0, 1), in parallel ----
+#ifdef LORA_FUSED_NOEST  // profiling ablation (results invalid): no estimate / sync
+    if (tid == 0) sp = FrameParams{0.0f, 0.0f, 0.0f, scale, 0, scaled, 0, 0};
+    if (false) {
+#else
+    if (est_lane) {
+#endif
+      cf in[P], z[P];
+      cf* row = er + wv * ROW;
+      lds_points<SF>(frame, wv, 0, l, scale, in);
+      rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, false, nullptr, l);
+      const uint64_t key = group_max(fft_key<SF, true, 0>(z, row, l, b), T);
+      if (l == 0) {
+        const uint32_t idx = key_index(key);
+        const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
+        float pw, fi;
+        detect_tail(key_value(key), row[lds_slot<SF>((int)im1)], row[lds_slot<SF>((int)ip1)], a.power_scale, &pw,
+                    &fi);
+        // one phase (osr 1): the candidate is kept iff p > best_p = -1e30 (LoRaDemod.cpp:
+        // 87,101), else the defaults (index 0, fIndex 0, bin 0) stand
+        EstCand c;
+        c.take = pw > -1e30f;
+        c.idx = c.take ? idx : 0u;
+        c.fi = c.take ? fi : 0.0f;
+        c.bin = c.take ? row[lds_slot<SF>((int)idx)] : cf{0.0f, 0.0f};
+        c.pad = 0;
+        ec[wv] = c;
+      }
+    }
+    lds_barrier();
+    FSTAMP(it, 2);
+    if (tid == 0) {  // LoRaDemod.cpp:111-138, symbols in order
+      float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
+#ifndef LORA_FUSED_NOEST
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const EstCand c = ec[s];
+        sum_index += (float)c.idx + c.fi;  // best_t = 0
+        const float phase = lm_atan2f(c.bin.im, c.bin.re);
+        if (s > 0) {
+          float d = phase - prev_phase;
+          while (d > PI_F) d -= 2.0f * PI_F;
+          while (d < -PI_F) d += 2.0f * PI_F;
+          phase_diff += d;
+        }
+        prev_phase = phase;
+      }
+#endif
+      const float avg_index = sum_index / 2.0f;
+      const float cfo_coarse = avg_index / (float)N;
+      const float cfo_fine = (phase_diff / 1.0f) / (2.0f * PI_F * (float)N);
+      const float cfo = cfo_coarse + cfo_fine;
+      const float frac = avg_index - floorf(avg_index + 0.5f);
+      const float toff = 0.0f / 2.0f - frac * (float)N * 1.0f;  // avg_t = sum_t / 2 = 0
+      FrameParams q;
+      q.cfo = cfo;
+      q.toff = toff;
+      q.t_off = (int)roundf(toff);
+      q.rate = -2.0f * PI_F * cfo / (float)N;
+      q.scale = scale;
+      q.scaled = scaled;
+      q.pad0 = q.pad1 = 0;
+      sp = q;
+      if (a.cfo) a.cfo[f] = cfo;
+      if (a.toff) a.toff[f] = toff;
+      if (a.max_amp) a.max_amp[f] = maxv;
+    }
+    lds_barrier();
+    FSTAMP(it, 3);
+    const FrameParams q = sp;
+
+    // ---- sync symbol w on group 0 of wave w; its reads precede the first round's barrier ----
+#ifdef LORA_FUSED_NOSYNC  // profiling ablation (results invalid)
+    if (false) {
+#else
+    if (est_lane) {
+#endif
+      int64_t base;
+      int cg;
+      sym_base(wv, N, len, q.t_off, base, cg);
+      const float start = q.rate * ((float)((uint32_t)wv * (uint32_t)N) + (float)q.t_off / 1.0f);
+      cf in[P], z[P];
+      lds_points<SF>(frame, wv, (int)(base - (int64_t)wv * N), l, scale, in);
+      rotate_place<SF, true, 0>(in, z, start, q.rate, false, nullptr, l);
+      const uint64_t key = group_max(fft_key<SF, false, 0>(z, er + wv * ROW, l, b), T);
+      if (l == 0) swl[wv] = key_index(key);
+    }
+    FSTAMP(it, 4);
+
+    // ---- data symbols ----
+#ifdef LORA_FUSED_NODATA  // profiling ablation (results invalid): no data symbols
+    const int per = 0;
+#else
+    const int per = a.total - 2;
+#endif
+    const int spb = nthr / T;
+    const bool down = q.t_off < 0;
+    for (int r0 = 0; r0 < per; r0 += spb) {
+      const int k = r0 + g;
+      const bool valid = k < per;
+      const int s = 2 + (down ? per - 1 - k : k);
+      cf in[P], z[P];
+      if (valid) {
+        int64_t base;
+        int cg;
+        sym_base(s, N, len, q.t_off, base, cg);
+        const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / 1.0f);
+        lds_points<SF>(frame, s, (int)(base - (int64_t)s * N), l, scale, in);
+        rotate_place<SF, true, 0, FAST>(in, z, start, q.rate, false, nullptr, l);
+      }
+      lds_barrier();  // every read of this round precedes the in-place transposes
+      if (valid) {
+        const uint64_t key = group_max(fft_key<SF, false, 0>(z, frame + s * ROW, l, b), T);
+        if (l == 0 && a.syms) a.syms[f * a.sym_stride + (s - 2)] = (uint16_t)key_index(key);
+      }
+    }
+    FSTAMP(it, 5);
+    lds_barrier();  // the frame's LDS is reloaded next; swl complete
+    FSTAMP(it, 6);
+    if (tid == 0 && a.sync) {
+      constexpr unsigned shift = SF - 4;
+      a.sync[f] = (uint8_t)((((swl[0] >> shift) & 0x0f) << 4) | ((swl[1] >> shift) & 0x0f));
+    }
+  }
+}
+
+template <int SF, int MODE, bool FAST>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+LORA_SCALAR_FP32 k_frame_fused(KArgs a, int nrows, int64_t frames, int stagger_ticks) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float wmax[8];
+  __shared__ FrameParams sp;
+  __shared__ EstCand ec[2];
+  __shared__ uint32_t swl[2];
+  (void)stagger_ticks;
+  fused_frame<SF, MODE, FAST>(a, nrows, blockIdx.x, smem, wmax, sp, ec, swl, 0);
+}
+
+template <int SF, int MODE, bool FAST>
+bool launch_fused_mode(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st) {
+  using G = Geo<SF>;
+  constexpr int T = G::T;
+  const int nrows = (int)((a.frame_len + G::N - 1) / G::N);
+  const size_t lds = sizeof(cf) * (size_t)(nrows + 2) * lds_row<SF>() + FusedTables<SF>::BYTES;
+  if (lds > lds_max) return false;
+  const void* fn = (const void*)k_frame_fused<SF, MODE, FAST>;
+  if (lds > 64 * 1024)
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
+  // one round of data symbols per frame when it fits 512 threads (>= 2 waves: the
+  // estimate runs symbols 0 and 1 on waves 0 and 1)
+  const int64_t want = (int64_t)(a.total - 2) * T;
+  int block = 128;
+  while (block < 512 && block < want) block *= 2;
+  // persistent: as many workgroups as fit at once, each looping over frames
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds) != hipSuccess || per_cu < 1)
+    return false;
+  const int64_t grid = frames;
+  static const int stagger = [] {  // 100 MHz ticks (LORA_MI355X_STAGGER, default 3 us)
+    const char* e = std::getenv("LORA_MI355X_STAGGER");
+    return e ? std::atoi(e) : 300;
+  }();
+  hipLaunchKernelGGL((k_frame_fused<SF, MODE, FAST>), dim3((unsigned)grid), dim3(block), lds, st, a, nrows, frames,
+                     per_cu >= 2 ? stagger : 0);
+  return true;
+}
+
+template <int SF>
+bool launch_fused_sf(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st) {
+  if (a.fast_rot)
+    return a.dechirp ? launch_fused_mode<SF, 0, true>(a, frames, lds_max, st)
+                     : launch_fused_mode<SF, 1, true>(a, frames, lds_max, st);
+  return a.dechirp ? launch_fused_mode<SF, 0, false>(a, frames, lds_max, st)
+                   : launch_fused_mode<SF, 1, false>(a, frames, lds_max, st);
+}
+
 template <int SF>
 int row_complex() {
   return lds_row<SF>();
@@ -872,6 +1233,29 @@ bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
 }
 
 }  // namespace
+
+#ifdef LORA_FUSED_TIMING
+extern "C" int lora_debug_fused_timing(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_dbg), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -5;
+}
+extern "C" int lora_debug_fused_timing_clear(void) {
+  static unsigned long long zeros[2048 * 16 * 8];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fused_dbg), zeros, sizeof(zeros)) == hipSuccess ? 0 : -5;
+}
+#endif
+
+bool launch_fused(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st) {
+  const bool simple = a.mode == LORA_MODE_LEGACY && a.osr == 1 && !a.hann && a.have_sync && a.total >= 2;
+  if (!simple || a.est_only || a.ablate || frames <= 0 || frames >= (int64_t(1) << 31)) return false;
+  // 16-byte loads: every frame starts 16-byte aligned
+  if ((a.frame_stride & 1) || (reinterpret_cast<uintptr_t>(a.iq) & 15)) return false;
+  switch (a.sf) {
+    case 6: return launch_fused_sf<6>(a, frames, lds_max, st);
+    case 7: return launch_fused_sf<7>(a, frames, lds_max, st);
+    case 8: return launch_fused_sf<8>(a, frames, lds_max, st);
+    default: return false;
+  }
+}
 
 bool launch_est_fast(const KArgs& a, int64_t frames, hipStream_t st) {
   if (a.total < 2 || a.est_only || a.mode == LORA_MODE_RAW) return false;

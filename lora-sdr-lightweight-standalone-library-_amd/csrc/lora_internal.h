@@ -68,6 +68,11 @@ __device__ __forceinline__ float frame_maxv(const KArgs& a, int64_t f) {
 // Returns false if the configuration is not covered (caller uses the generic kernel).
 bool launch_demod_fast(const KArgs& a, int s0, int64_t work, hipStream_t st);
 
+// Frame-resident single-read pipeline (max + estimate + every symbol in one launch, the
+// frame staged in LDS) for LEGACY osr-1 unwindowed frames of SF 6-8 whose LDS image is at
+// most lds_max bytes; false = not covered (caller runs the three-launch path).
+bool launch_fused(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st);
+
 // Offset estimate + sync symbols with the same FFT machinery, one lane group per frame
 // (frames with >= 2 whole symbols; false = not covered, use k_estimate).
 bool launch_est_fast(const KArgs& a, int64_t frames, hipStream_t st);

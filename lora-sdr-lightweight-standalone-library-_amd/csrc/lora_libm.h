@@ -23,6 +23,24 @@
 //
 // Contraction must be OFF wherever this header is compiled (hipcc defaults to
 // -ffp-contract=fast-honor-pragmas; the pragma below pins it).
+//
+// Third-party notices for the algorithms and constants restated here:
+//
+//   sincosf, logf (Arm optimized-routines, as shipped in glibc 2.35):
+//     Copyright (c) 2018-2019, Arm Limited.
+//     SPDX-License-Identifier: MIT (optimized-routines; glibc carries it under
+//     LGPL-2.1-or-later)
+//
+//   atanf, atan2f, log10f (fdlibm, as shipped in glibc 2.35 sysdeps/ieee754/flt-32):
+//     Conversion to float by Ian Lance Taylor, Cygnus Support, ian@cygnus.com.
+//     ====================================================
+//     Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//
+//     Developed at SunPro, a Sun Microsystems, Inc. business.
+//     Permission to use, copy, modify, and distribute this
+//     software is freely granted, provided that this notice
+//     is preserved.
+//     ====================================================
 #pragma once
 #include <stdint.h>
 

@@ -25,6 +25,9 @@ LORA_MODE_LEGACY = 0
 LORA_MODE_API = 1
 LORA_MODE_RAW = 2
 
+# lora_demod_last_kernels bits
+KERNEL_BITS = {"frame_max": 1, "estimate": 2, "demod": 4, "fused": 8, "generic": 16}
+
 # Every symbol include/lora_mi355x.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (
     "lora_demod_plan_create",
@@ -37,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "lora_compensate_offsets_batch",
     "lora_demod_profile_enable",
     "lora_demod_profile_read",
+    "lora_demod_last_kernels",
     "lora_last_error",
     "lora_version",
 )
@@ -112,6 +116,8 @@ def lib() -> C.CDLL:
     L.lora_demod_profile_enable.argtypes = [C.c_void_p, C.c_int]
     L.lora_demod_profile_read.restype = C.c_int
     L.lora_demod_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)]
+    L.lora_demod_last_kernels.restype = C.c_int
+    L.lora_demod_last_kernels.argtypes = [C.c_void_p]
     L.lora_last_error.restype = C.c_char_p
     L.lora_version.restype = C.c_char_p
     _lib = L

@@ -44,6 +44,32 @@ def _require_cuda(t: torch.Tensor, name: str) -> None:
                         "CPU fallback")
 
 
+def _check_buf(t: torch.Tensor, name: str, dtype: torch.dtype, device: torch.device, numel: int) -> None:
+    """Everything the C library cannot check about a raw pointer: a wrong device, dtype,
+    stride or length would be a GPU memory fault or silent corruption, not an error."""
+    _require_cuda(t, name)
+    if t.device != device:
+        raise ValueError(f"{name} is on {t.device}, the plan is on {device}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if numel > 0 and (not t.is_contiguous() or t.numel() < numel):
+        raise ValueError(f"{name} must be contiguous with >= {numel} elements "
+                         f"(got {t.numel()}, contiguous={t.is_contiguous()})")
+
+
+def _check_iq(iq: torch.Tensor, device: torch.device) -> torch.Tensor:
+    _require_cuda(iq, "iq")
+    if iq.device != device:
+        raise ValueError(f"iq is on {iq.device}, the plan is on {device}")
+    if iq.dtype != torch.complex64:
+        raise TypeError("iq must be complex64 (interleaved fp32 I/Q)")
+    if iq.dim() == 1:
+        iq = iq.unsqueeze(0)
+    if iq.dim() != 2 or (iq.shape[1] > 1 and iq.stride(1) != 1) or (iq.shape[0] > 1 and iq.stride(0) < iq.shape[1]):
+        raise ValueError("iq must be [frames, samples] with unit sample stride and non-overlapping rows")
+    return iq
+
+
 class DemodPlan:
     """A device plan for one demodulator configuration (lora_demod_init equivalent)."""
 
@@ -69,7 +95,11 @@ class DemodPlan:
         h = C.c_void_p()
         _capi.check(self._lib.lora_demod_plan_create(C.byref(prm), C.byref(h)))
         self._h = h
-        self._ws: Optional[torch.Tensor] = None
+        # Workspaces per stream (two streams never share frame maxima / FrameParams);
+        # ones used while a HIP graph was being captured are kept for the plan's lifetime,
+        # since the graph replays with their addresses.
+        self._ws: dict = {}
+        self._ws_captured: list = []
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -85,21 +115,28 @@ class DemodPlan:
     def symbols_per_frame(self, frame_len: int) -> int:
         return _capi.check(self._lib.lora_demod_symbols_per_frame(self._h, int(frame_len)))
 
+    def last_kernels(self) -> set:
+        """Kernels the last run() launched: {"fused"} for the frame-resident single-read
+        path, {"frame_max", "estimate", "demod"} for the three-launch path (+"generic")."""
+        m = self._lib.lora_demod_last_kernels(self._h)
+        return {k for k, b in _capi.KERNEL_BITS.items() if m & b}
+
     def _workspace(self, frames: int) -> torch.Tensor:
         need = self._lib.lora_demod_workspace_bytes(self._h, int(frames))
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
-        return self._ws
+        key = _stream_handle(self.device)
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < need:
+            # allocated on (and stream-ordered with) the current stream, so dropping the
+            # smaller one is safe for work already queued on it
+            ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+            if torch.cuda.is_current_stream_capturing():
+                self._ws_captured.append(ws)
+        return ws
 
     def run(self, iq: torch.Tensor, out: Optional[DemodResult] = None) -> DemodResult:
         """Demodulate a [F, L] (or [L]) complex64 CUDA tensor; one frame per row."""
-        _require_cuda(iq, "iq")
-        if iq.dtype != torch.complex64:
-            raise TypeError("iq must be complex64 (interleaved fp32 I/Q)")
-        if iq.dim() == 1:
-            iq = iq.unsqueeze(0)
-        if iq.dim() != 2 or iq.stride(1) != 1:
-            raise ValueError("iq must be [frames, samples] with unit sample stride")
+        iq = _check_iq(iq, self.device)
         F, L = iq.shape
         S = self.symbols_per_frame(L)
         dev = self.device
@@ -110,6 +147,15 @@ class DemodPlan:
                 cfo=torch.empty(F, dtype=torch.float32, device=dev),
                 time_offset=torch.empty(F, dtype=torch.float32, device=dev),
                 max_amp=torch.zeros(F, dtype=torch.float32, device=dev))
+        else:
+            if S > 0:
+                _require_cuda(out.symbols, "out.symbols")
+                if (out.symbols.dtype != torch.uint16 or out.symbols.device != dev or out.symbols.dim() != 2
+                        or out.symbols.shape[0] < F or out.symbols.shape[1] < S or out.symbols.stride(1) != 1):
+                    raise ValueError(f"out.symbols must be a uint16 [>={F}, >={S}] tensor on {dev}")
+            for name, dt in (("sync", torch.uint8), ("cfo", torch.float32), ("time_offset", torch.float32),
+                             ("max_amp", torch.float32)):
+                _check_buf(getattr(out, name), "out." + name, dt, dev, F)
         ws = self._workspace(F)
         o = _capi.DemodOutputs(out.symbols.data_ptr() if S > 0 else None,
                                out.symbols.stride(0) if S > 0 else 0,
@@ -122,10 +168,10 @@ class DemodPlan:
 
     def estimate_offsets(self, iq: torch.Tensor, cfo: torch.Tensor, time_offset: torch.Tensor) -> int:
         """phy.cpp:78-145 over every whole symbol of each frame (raw samples)."""
-        _require_cuda(iq, "iq")
-        if iq.dim() == 1:
-            iq = iq.unsqueeze(0)
+        iq = _check_iq(iq, self.device)
         F, L = iq.shape
+        _check_buf(cfo, "cfo", torch.float32, self.device, F)
+        _check_buf(time_offset, "time_offset", torch.float32, self.device, F)
         stride = iq.stride(0) if F > 1 else L
         return _capi.check(self._lib.lora_estimate_offsets_batch(
             self._h, iq.data_ptr(), F, L, stride, cfo.data_ptr(), time_offset.data_ptr(),
@@ -137,9 +183,10 @@ def compensate_offsets(iq: torch.Tensor, sf: int, osr: int, cfo: torch.Tensor,
     """phy.cpp:147-176 for a [F, L] batch; returns a new tensor (out of place)."""
     _require_cuda(iq, "iq")
     squeeze = iq.dim() == 1
-    x = iq.unsqueeze(0) if squeeze else iq
-    x = x.contiguous()
+    x = _check_iq((iq.unsqueeze(0) if squeeze else iq).contiguous(), iq.device)
     F, L = x.shape
+    _check_buf(cfo, "cfo", torch.float32, x.device, F)
+    _check_buf(time_offset, "time_offset", torch.float32, x.device, F)
     out = torch.empty_like(x)
     lib = _capi.lib()
     _capi.check(lib.lora_compensate_offsets_batch(
@@ -156,11 +203,27 @@ class LoRaDemod:
 
     ``work(iq)`` consumes one frame (or a [F, L] batch) of raw IQ and returns the
     symbol stream; per-frame metrics of the last call are in ``last``.
+
+    The Pothos-only parameters (the upstream block is an empty submodule in the
+    reference, so their semantics are not pinned by any reference code):
+      * ``mtu`` - the most data symbols one frame (packet) yields: ``work`` returns at
+        most ``mtu`` symbols per frame (the first ones); ``last`` keeps them all.
+      * ``thresh`` - a detection threshold in dB.  The reference library path
+        (LoRaDemod.cpp:49-195) has no detection gate, so no gate is applied; only the
+        graph's value -30.0 (examples/lora_simulation.pth:440) is accepted, and any
+        other value raises instead of being silently ignored.
     """
+
+    THRESH_DEFAULT = -30.0
 
     def __init__(self, sf: int, sync: int = 0x12, thresh: float = -30.0, mtu: int = 256,
                  bw: int = 125000, cr: int = 1, osr: int = 1, window="none",
                  dechirp: bool = True, mode: str = "legacy", device=None, precision: str = "exact"):
+        if float(thresh) != self.THRESH_DEFAULT:
+            raise ValueError(f"thresh={thresh}: no detection gate is defined by the reference path; "
+                             f"only the default {self.THRESH_DEFAULT} is accepted")
+        if int(mtu) < 1:
+            raise ValueError("mtu must be >= 1 symbol")
         self.sf, self.sync, self.thresh, self.mtu = int(sf), int(sync) & 0xFF, float(thresh), int(mtu)
         self.bw, self.cr, self.osr = int(bw), int(cr), int(osr) if osr else 1
         self.plan = DemodPlan(sf, self.osr, bw, window, dechirp, mode, device, precision)
@@ -169,7 +232,8 @@ class LoRaDemod:
     def work(self, iq: torch.Tensor) -> torch.Tensor:
         res = self.plan.run(iq)
         self.last = res
-        return res.symbols[0] if iq.dim() == 1 else res.symbols
+        syms = res.symbols[:, :self.mtu]
+        return syms[0] if iq.dim() == 1 else syms
 
     def work_frames(self, iq: torch.Tensor) -> DemodResult:
         self.last = self.plan.run(iq)

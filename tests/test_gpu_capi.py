@@ -103,3 +103,50 @@ def test_no_device_allocation_per_call(amd):
     torch.cuda.synchronize()
     assert torch.cuda.memory_stats()["allocation.all.allocated"] == before
     assert torch.equal(out.symbols.to(torch.int32).cpu(), syms)
+
+
+def test_wrapper_rejects_bad_tensors(amd):
+    """The ctypes wrappers check what the C library cannot: a CPU, wrong-dtype,
+    strided or short tensor raises instead of reaching a kernel as a raw pointer."""
+    plan = amd.DemodPlan(7)
+    F, L = 4, 20 * 128
+    iq = torch.zeros((F, L), dtype=torch.complex64, device="cuda")
+    with pytest.raises(TypeError):
+        plan.run(iq.cpu())
+    with pytest.raises(TypeError):
+        plan.run(torch.zeros((F, 2 * L), dtype=torch.float32, device="cuda"))
+    with pytest.raises(ValueError):
+        plan.run(torch.zeros((L, F), dtype=torch.complex64, device="cuda").t())
+    cfo = torch.zeros(F, dtype=torch.float32, device="cuda")
+    toff = torch.zeros(F, dtype=torch.float32, device="cuda")
+    with pytest.raises(TypeError):
+        plan.estimate_offsets(iq, cfo.cpu(), toff)
+    with pytest.raises(TypeError):
+        plan.estimate_offsets(iq, cfo.double(), toff)
+    with pytest.raises(ValueError):
+        plan.estimate_offsets(iq, cfo[:2], toff)
+    with pytest.raises(ValueError):
+        amd.compensate_offsets(iq, 7, 1, cfo, toff[:1])
+    with pytest.raises(TypeError):
+        amd.compensate_offsets(iq, 7, 1, cfo.half(), toff)
+    res = plan.run(iq)
+    res.cfo = res.cfo[:1]
+    with pytest.raises(ValueError):
+        plan.run(iq, out=res)
+    assert plan.estimate_offsets(iq, cfo, toff) == 20
+
+
+def test_workspace_per_stream(amd):
+    """Runs on two streams use two workspaces (no shared frame maxima / FrameParams)."""
+    plan = amd.DemodPlan(7, dechirp=True)
+    iq = amd.modulate(torch.randint(0, 128, (64, 64), device="cuda", dtype=torch.int32), 7)
+    ref = plan.run(iq).symbols.clone()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        r1 = plan.run(iq)
+    with torch.cuda.stream(s2):
+        r2 = plan.run(iq)
+    torch.cuda.synchronize()
+    assert len(plan._ws) >= 3
+    assert torch.equal(r1.symbols, ref) and torch.equal(r2.symbols, ref)

@@ -85,23 +85,28 @@ CASES = [  # (sf, osr, hann, dechirp, F, symbols-per-frame, extra samples, kind)
 
 
 def make_plan(amd, path, *args, **kw):
-    """path "fast": register-blocked kernels (LDS passes read slot-major twiddle copies);
-    "gather": the same kernels gathering twiddles from the natural table
-    (LORA_MI355X_TWT=0); "generic": LDS reference kernel (A/B)."""
+    """path "fast": register-blocked kernels (LDS passes read slot-major twiddle copies),
+    with the frame-resident single-read kernel wherever it covers the configuration;
+    "split": the same without the frame-resident kernel (three launches,
+    LORA_MI355X_FUSED=0); "gather": the fast kernels gathering twiddles from the natural
+    table (LORA_MI355X_TWT=0); "generic": LDS reference kernel (A/B)."""
     import os
 
     if path == "generic":
         os.environ["LORA_MI355X_GENERIC"] = "1"
     if path == "gather":
         os.environ["LORA_MI355X_TWT"] = "0"
+    if path == "split":
+        os.environ["LORA_MI355X_FUSED"] = "0"
     try:
         return amd.DemodPlan(*args, **kw)
     finally:
         os.environ.pop("LORA_MI355X_GENERIC", None)
         os.environ.pop("LORA_MI355X_TWT", None)
+        os.environ.pop("LORA_MI355X_FUSED", None)
 
 
-@pytest.mark.parametrize("path", ["fast", "gather", "generic"])
+@pytest.mark.parametrize("path", ["fast", "split", "gather", "generic"])
 @pytest.mark.parametrize("case", CASES, ids=[f"sf{c[0]}-osr{c[1]}-h{int(c[2])}-d{int(c[3])}-{c[7]}-S{c[5]}"
                                              for c in CASES])
 def test_legacy_demod_matches_oracle(O, amd, case, path):
