@@ -354,3 +354,91 @@ def decode_with_crc(symbols):
         provided = int(out[n - 2]) | (int(out[n - 1]) << 8)
         return out, provided == sx1272_data_checksum(out[2:n - 2].tobytes())
     return out, False
+
+
+# ---------------------------------------------------------------------------
+# The coding chain around the demodulator, per coding rate 4/(4+RDD): nibble codes,
+# whitening, diagonal interleave, Gray mapping (LoRaCodes.hpp:176-189, 201-222,
+# 229-371, 376-412), in the order of the LoRa-SDR encoder the reference ports (runners/
+# lora_phy_vector_generate.cpp:189-223 uses the RDD = 4 case with Hamming 8/4).
+# ---------------------------------------------------------------------------
+
+
+def rdd_of(cr) -> int:
+    """'4/5'..'4/8' -> RDD 1..4, '4/4' -> 0; an integer CR index 1..4 is RDD itself."""
+    s = str(cr)
+    if "/" in s:
+        num, den = s.split("/")
+        rdd = int(den) - int(num)
+    else:
+        rdd = int(s)
+    if not 0 <= rdd <= 4:
+        raise ValueError(f"coding rate {cr!r}: RDD must be 0..4")
+    return rdd
+
+
+def nibble_encode(nibbles, rdd: int) -> np.ndarray:
+    """Nibble -> codeword: RDD 4 Hamming 8/4, 3 Hamming 7/4, 2 parity 6/4, 1 parity 5/4,
+    0 the bare nibble."""
+    x = np.asarray(nibbles, np.int64) & 0xF
+    if rdd == 4:
+        return encode_hamming84(x)
+    if rdd == 3:
+        return encode_hamming74(x)
+    if rdd == 2:
+        return encode_parity64(x)
+    if rdd == 1:
+        return encode_parity54(x)
+    return x.astype(np.uint8)
+
+
+def nibble_decode(codewords, rdd: int):
+    """Codeword -> (nibble, error) with the decoder of nibble_encode's code (Hamming 8/4's
+    'bad' flag is folded into error)."""
+    b = np.asarray(codewords, np.int64) & 0xFF
+    if rdd == 4:
+        n, e, bad = decode_hamming84(b)
+        return n & 0xF, e | bad
+    if rdd == 3:
+        n, e = decode_hamming74(b)
+        return n & 0xF, e
+    if rdd == 2:
+        return check_parity64(b)
+    if rdd == 1:
+        return check_parity54(b)
+    return (b & 0xF).astype(np.uint8), np.zeros(b.shape, bool)
+
+
+def payload_nibbles(payload) -> np.ndarray:
+    """Bytes -> nibbles, high nibble first (lora_phy_vector_generate.cpp:196-199)."""
+    b = np.frombuffer(bytes(payload), np.uint8).astype(np.int64)
+    out = np.empty(2 * len(b), np.int64)
+    out[0::2] = b >> 4
+    out[1::2] = b & 0xF
+    return out
+
+
+def encode_chain(payload, sf: int, rdd: int):
+    """TX side: nibbles -> codewords (padded with zero codewords to a multiple of
+    PPM = sf) -> whitening -> diagonal interleave -> Gray.  Returns the stages as a dict
+    (codewords, whitened, interleaved, symbols)."""
+    cw = nibble_encode(payload_nibbles(payload), rdd).astype(np.uint8)
+    n = -(-len(cw) // sf) * sf
+    cw = np.concatenate([cw, np.zeros(n - len(cw), np.uint8)])
+    wh = np.frombuffer(sx1272_whitening_lfsr(cw.tobytes(), 0, rdd), np.uint8)
+    il = diagonal_interleave(wh, sf, rdd)
+    return {"codewords": cw, "whitened": wh, "interleaved": il, "symbols": binary_to_gray16(il)}
+
+
+def decode_chain(symbols, sf: int, rdd: int, nbytes: int):
+    """RX side, the inverse of encode_chain: Gray demap -> diagonal deinterleave ->
+    de-whitening -> nibble decode -> bytes.  Returns the stages (binary, deinterleaved,
+    dewhitened, nibbles, errors, payload)."""
+    bi = gray_to_binary16(symbols)
+    di = diagonal_deinterleave(bi, sf, rdd)
+    dw = np.frombuffer(sx1272_whitening_lfsr(di.tobytes(), 0, rdd), np.uint8)
+    nib, err = nibble_decode(dw, rdd)
+    nib = nib[: 2 * nbytes].astype(np.int64)
+    pay = ((nib[0::2] << 4) | nib[1::2]).astype(np.uint8)
+    return {"binary": bi, "deinterleaved": di, "dewhitened": dw, "nibbles": nib.astype(np.uint8),
+            "errors": err, "payload": pay}
