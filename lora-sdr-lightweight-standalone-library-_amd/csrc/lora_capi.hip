@@ -4,8 +4,10 @@
 // Demodulation of F frames is three launches on one stream (generic path, any SF
 // 2..12, any osr, any frame length):
 //   k_frame_max  LEGACY only: per-frame max(|I|,|Q|) of the (dechirped) samples,
-//                LoRaDemod.cpp:59-67, streamed with 16-byte loads, one atomicMax per
-//                workgroup.
+//                LoRaDemod.cpp:59-67, streamed with 16-byte loads; each block writes its
+//                partial maximum to its own workspace slot (no atomics, no zeroing) and
+//                the estimate reduces a frame's partials (k_frame_max_wave: one wave,
+//                one partial per short frame).
 //   k_estimate   one workgroup per frame: the 2-symbol x osr-phase offset estimate
 //                (LoRaDemod.cpp:79-135 / phy.cpp:78-145) and the two sync symbols,
 //                leaving cfo / t_off / rate / scale in the workspace.
@@ -62,9 +64,11 @@ using lora::PI_F;
 // exact formulas and the host libm, so the device sees the reference's constants).
 // ---------------------------------------------------------------------------------
 
+}  // namespace
+
 // ChirpGenerator.hpp:105-132 (genChirp), float recurrence, std::polar -> sincosf.
-void host_gen_chirp(std::complex<float>* out, int N, int osr, int NN, float f0, bool down,
-                    float ampl, float& phase, float bw_scale) {
+void lora::host_gen_chirp(std::complex<float>* out, int N, int osr, int NN, float f0, bool down,
+                          float ampl, float& phase, float bw_scale) {
   const float fMin = -M_PI * bw_scale / osr;
   const float fMax = M_PI * bw_scale / osr;
   const float fStep = (2 * M_PI * bw_scale) / (N * osr * osr);
@@ -82,6 +86,9 @@ void host_gen_chirp(std::complex<float>* out, int N, int osr, int NN, float f0, 
   }
   phase -= std::floor(phase / (2 * M_PI)) * 2 * M_PI;
 }
+
+namespace {
+using lora::host_gen_chirp;
 
 // kissfft.hh:81-97: radix plan; only 4/2 radices occur for powers of two.
 std::vector<int> fft_radices(int nfft) {
@@ -686,7 +693,18 @@ struct ProfScope {
 
 extern "C" {
 
-const char* lora_version(void) { return "lora_mi355x 0.1 (gfx950)"; }
+#ifndef LORA_SRC_HASH
+#define LORA_SRC_HASH "unknown"
+#endif
+#ifndef LORA_GIT_HASH
+#define LORA_GIT_HASH "unknown"
+#endif
+// "src=" is the sha256 (first 16 hex digits) of the library's sources as the Makefile
+// hashed them at build time; smoke() recomputes it from the tree it runs in, so a stale
+// prebuilt library cannot pass for the current sources.
+const char* lora_version(void) {
+  return "lora_mi355x 0.2 (gfx950) src=" LORA_SRC_HASH " git=" LORA_GIT_HASH;
+}
 
 const char* lora_last_error(void) { return g_last_error.c_str(); }
 
@@ -778,6 +796,9 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
     plan->use_fast = (g && g[0] == '1') ? 0 : 1;
     const char* ab = std::getenv("LORA_MI355X_ABLATE");
     plan->ablate = ab ? std::atoi(ab) : 0;
+    if (plan->ablate)
+      std::fprintf(stderr, "lora_mi355x: LORA_MI355X_ABLATE=%d - profiling ablation, demodulation results are "
+                           "INVALID for this plan\n", plan->ablate);
     const char* ch = std::getenv("LORA_MI355X_CHUNKS");
     plan->max_chunks = std::max(1, std::min(kMaxChunks, ch ? std::atoi(ch) : 1));
     // Frame-resident single-read kernel (k_frame_fused), opt-in: LORA_MI355X_FUSED = its LDS

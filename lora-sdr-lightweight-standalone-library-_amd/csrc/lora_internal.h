@@ -1,5 +1,7 @@
 // lora_internal.h — kernel argument block shared by the demod translation units.
 #pragma once
+#include <complex>
+
 #include "lora_device.h"
 
 namespace lora {
@@ -63,6 +65,11 @@ __device__ __forceinline__ float frame_maxv(const KArgs& a, int64_t f) {
   for (int c = 0; c < a.mx_bpf; ++c) m = fmaxf(m, __uint_as_float(a.maxbits[f * a.mx_bpf + c]));
   return m;
 }
+
+// ChirpGenerator.hpp:105-132 genChirp on the host (the fp32 recurrence, glibc sincosf):
+// the plan's down-chirp tables and the C++ drop-in's genChirp (lora_phy_dropin.cpp).
+void host_gen_chirp(std::complex<float>* out, int N, int osr, int NN, float f0, bool down, float ampl,
+                    float& phase, float bw_scale);
 
 // Fast symbol demodulator (lora_demod_fast.hip): register-blocked kissfft-exact FFT.
 // Returns false if the configuration is not covered (caller uses the generic kernel).

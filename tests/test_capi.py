@@ -94,3 +94,25 @@ def test_product_path_has_no_cpu_fallback():
         amd.DemodPlan(7)
     with pytest.raises(TypeError):
         amd.modulate(torch.zeros(4, dtype=torch.int32), 7)
+
+
+def test_library_built_from_these_sources():
+    """lora_version()'s src= stamp equals the hash of the sources in this tree (a stale
+    prebuilt liblora_mi355x.so would fail here and in smoke())."""
+    import lora_phy_amd
+
+    v = lora_phy_amd.check_build()
+    assert "git=" in v and "(gfx950)" in v
+
+
+def test_lora_demod_thresh_and_mtu_validation():
+    """Pothos-only parameters (examples/lora_simulation.pth:440,444): thresh has no gate in
+    the reference path, so a non-default value raises instead of being ignored; mtu >= 1."""
+    import pytest as _pytest
+
+    import lora_phy_amd
+
+    with _pytest.raises(ValueError):
+        lora_phy_amd.LoRaDemod(7, thresh=-20.0)
+    with _pytest.raises(ValueError):
+        lora_phy_amd.LoRaDemod(7, mtu=0)

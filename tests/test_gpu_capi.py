@@ -150,3 +150,13 @@ def test_workspace_per_stream(amd):
     torch.cuda.synchronize()
     assert len(plan._ws) >= 3
     assert torch.equal(r1.symbols, ref) and torch.equal(r2.symbols, ref)
+
+
+def test_lora_demod_mtu_caps_symbols_per_frame(amd):
+    syms = torch.randint(0, 128, (4, 30), device="cuda", dtype=torch.int32)
+    iq = amd.modulate(syms, 7)
+    d = amd.LoRaDemod(7, mtu=20)
+    out = d.work(iq)
+    assert out.shape == (4, 20)
+    assert torch.equal(out.to(torch.int32), syms[:, :20])
+    assert d.last.symbols.shape == (4, 30)
