@@ -176,6 +176,7 @@ int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls);
 #define LORA_KERNEL_DEMOD 4
 #define LORA_KERNEL_FUSED 8
 #define LORA_KERNEL_GENERIC 16
+#define LORA_KERNEL_FRAME_MAX_WAVE 32 /* with FRAME_MAX: the one-wave-per-frame variant (short frames) */
 int lora_demod_last_kernels(const lora_demod_plan* plan);
 
 /* Thread-local text of the last error ("" if none). */

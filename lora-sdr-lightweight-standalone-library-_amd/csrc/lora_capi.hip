@@ -1003,7 +1003,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   int kernels = 0;
   auto prep = [&](const KArgs& ac, uint32_t* mb, int64_t nf, hipStream_t s) {
     if (p.mode == LORA_MODE_LEGACY && frame_len > 0) {
-      kernels |= LORA_KERNEL_FRAME_MAX;
+      kernels |= LORA_KERNEL_FRAME_MAX | (max_wave ? LORA_KERNEL_FRAME_MAX_WAVE : 0);
       ProfScope ps(plan, 0, s);
       if (max_wave)
         hipLaunchKernelGGL(k_frame_max_wave, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, s, ac, nf, mb);
