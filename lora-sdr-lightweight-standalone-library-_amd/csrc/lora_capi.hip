@@ -587,17 +587,24 @@ __global__ void k_mod_phase(ModArgs a) {
   }
 }
 
-// One 64-lane workgroup per 64 chirps.  The genChirp recurrence (ChirpGenerator.hpp:
-// 118-128: f += fStep, wrap, phase += f, all fp32) is inherently sequential, so each
-// lane advances its own chirp 64 samples at a time into an LDS tile; the wave then
-// evaluates sincosf over the transposed tile, so that for every chirp 64 consecutive
-// samples (512 B) are stored by one coalesced instruction.
+// One wave per 64 chirps, four waves per workgroup.  The genChirp recurrence
+// (ChirpGenerator.hpp:118-128: f += fStep, wrap, phase += f, all fp32) is inherently
+// sequential, so each lane advances its own chirp kModBatch samples at a time into the
+// wave's LDS tile; the wave then evaluates sincosf over the transposed tile, four chirps
+// x 16 consecutive samples per store instruction (128-B segments).  The narrow tile
+// (64 x 17 floats per wave) keeps up to 8 waves per SIMD resident, which is what hides
+// the recurrence's dependent-add latency (the former 64 x 65 tile allowed ~2).
 constexpr int kModLanes = 64;
-__global__ void __launch_bounds__(kModLanes) k_mod_samples(ModArgs a) {
-  __shared__ float tile[kModLanes][kModLanes + 1];  // [chirp][sample], padded row
-  const int lane = threadIdx.x;
+constexpr int kModBatch = 16;
+constexpr int kModWaves = 4;
+__global__ void __launch_bounds__(kModLanes * kModWaves) k_mod_samples(ModArgs a) {
+  __shared__ float tiles[kModWaves][kModLanes][kModBatch + 1];  // [wave][chirp][sample]
+  const int lane = threadIdx.x & (kModLanes - 1);
+  const int wv = threadIdx.x / kModLanes;
+  float(*tile)[kModBatch + 1] = tiles[wv];
   const int64_t nch = a.frames * (int64_t)a.nchirp;
-  const int64_t w0 = (int64_t)blockIdx.x * kModLanes;
+  const int64_t w0 = ((int64_t)blockIdx.x * kModWaves + wv) * kModLanes;
+  if (w0 >= nch) return;  // whole waves exit together; no workgroup barrier below
   const int64_t w = w0 + lane;
   const bool valid = w < nch;
   const int64_t wc = valid ? w : nch - 1;
@@ -607,23 +614,29 @@ __global__ void __launch_bounds__(kModLanes) k_mod_samples(ModArgs a) {
   float f = a.fMin + chirp_f0(a, fr, c);
   const float span = a.fMax - a.fMin;
   const int nvalid = (int)min((int64_t)kModLanes, nch - w0);
-  for (int i0 = 0; i0 < a.step; i0 += kModLanes) {
-    const int cnt = min(kModLanes, a.step - i0);
-    for (int j = 0; j < cnt; ++j) {
+  // store role of this lane: chirp sub-row (lane >> 4) and sample (lane & 15)
+  const int sub = lane >> 4, j = lane & (kModBatch - 1);
+  for (int i0 = 0; i0 < a.step; i0 += kModBatch) {
+    const int cnt = min(kModBatch, a.step - i0);
+    for (int k = 0; k < cnt; ++k) {
       f += a.fStep;
       if (f > a.fMax) f -= span;
       phase += f;
-      tile[lane][j] = phase;
+      tile[lane][k] = phase;
     }
-    __syncthreads();  // single wave: orders the tile writes before the reads
-    if (lane < cnt) {
-      for (int ch = 0; ch < nvalid; ++ch) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (j < cnt) {
+      for (int ch = sub; ch < nvalid; ch += kModLanes / kModBatch) {
         float sn, cs;
-        lm_sincosf_bf(tile[ch][lane], &sn, &cs);
-        a.iq[(w0 + ch) * a.step + i0 + lane] = cf{a.ampl * cs, a.ampl * sn};
+        lm_sincosf_bf(tile[ch][j], &sn, &cs);
+        a.iq[(w0 + ch) * a.step + i0 + j] = cf{a.ampl * cs, a.ampl * sn};
       }
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -1127,7 +1140,9 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
   if (prev != device) HIP_TRY(hipSetDevice(device));
   hipLaunchKernelGGL(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, a);
   const int64_t chirps = frames * a.nchirp;
-  hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((chirps + 63) / 64)), dim3(64), 0, st, a);
+  const int64_t per_block = (int64_t)kModLanes * kModWaves;
+  hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((chirps + per_block - 1) / per_block)), dim3(per_block), 0, st,
+                     a);
   hipError_t e = hipGetLastError();
   if (prev != device) hipSetDevice(prev);
   if (e != hipSuccess) return set_error(LORA_EIO, std::string("mod launch: ") + hipGetErrorString(e));
