@@ -578,9 +578,13 @@ __global__ void k_mod_phase(ModArgs a) {
   for (int c = 0; c < a.nchirp; ++c) {
     out[(int64_t)c * a.step].re = phase;  // start phase, consumed by k_mod_samples
     float f = a.fMin + chirp_f0(a, fr, c);
+    // One lane per frame runs the whole chain: the kernel is bound by this loop's
+    // instruction count (one wave per SIMD issues a wave64 VALU op every 4 cycles), so
+    // it is unrolled - 5 VALU per sample, no scalar loop overhead (SF12: 7.9 -> ~3 ms).
+#pragma unroll 16
     for (int i = 0; i < a.step; ++i) {
       f += a.fStep;
-      if (f > a.fMax) f -= span;
+      f = f > a.fMax ? f - span : f;
       phase += f;
     }
     phase = (float)((double)phase - floor((double)phase / (2 * M_PI)) * 2 * M_PI);
