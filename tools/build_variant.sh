@@ -5,4 +5,4 @@
 set -e
 cd "$(dirname "$0")/../lora-sdr-lightweight-standalone-library-_amd"
 mkdir -p lora_phy_amd/lib/variants
-make -s ARCH=gfx950 OUT=lora_phy_amd/lib/variants/$1.so EXTRA="$2"
+make -s ARCH=gfx950 OUT=lora_phy_amd/lib/variants/$1.so EXTRA="$2" lora_phy_amd/lib/variants/$1.so
