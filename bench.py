@@ -88,7 +88,12 @@ def dist_setup(n_gpus, plumbing=False):
 
         ndev = torch.cuda.device_count()
         if local >= ndev:
-            raise SystemExit(f"bench.py: rank needs device {local} but {ndev} are visible")
+            if os.environ.get("LORA_BENCH_SHARE_DEVICES") == "1" and ndev > 0:
+                # rehearsal of the multi-rank path on a box with fewer GPUs than ranks:
+                # ranks share devices round-robin (numbers are then not per-GPU figures)
+                local = local % ndev
+            else:
+                raise SystemExit(f"bench.py: rank needs device {local} but {ndev} are visible")
         torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
