@@ -187,6 +187,7 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     for _ in range(warmup):
         out = plan.run(iq, out)
     torch.cuda.synchronize(device)
+    fixed0 = plan.spec_recomputed()
     barrier(dist)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
@@ -195,6 +196,8 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     torch.cuda.synchronize(device)
     barrier(dist)
     wall = time.perf_counter() - t0
+    fixed = (plan.spec_recomputed() - fixed0) / steps
+    kernels = sorted(plan.last_kernels())
     stage_ms, out = stage_times(plan, iq, out, steps, device)
     wall_max, units = all_max_sum(dist, wall, frames * data_syms * steps)
     total_syms = data_syms + 2
@@ -214,6 +217,7 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     return {
         "sf": sf, "frames": frames, "data_symbols": frames * data_syms, "iq_bytes": iq.numel() * 8,
         "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ser == 0.0, "ser_vs_tx": ser,
+        "kernels": kernels, "spec_recomputed_per_step": fixed,
         "msym_s_data": frames * data_syms / (ms_step * 1e-3) / 1e6,
         "msym_s_all_ranks": units / wall_max / 1e6, "ms_per_step_max_rank": wall_max * 1e3 / steps,
         "msym_s_all": frames * total_syms / (ms_step * 1e-3) / 1e6,
@@ -385,7 +389,8 @@ def fast_summary(r):
 def variant_summary(r, base, note):
     return {"note": note, "ms_per_step": r["ms_per_step"], "stage_ms": r["stage_ms"],
             "value_all_ranks_msym_s": r["msym_s_all_ranks"], "ser_vs_tx": r["ser_vs_tx"],
-            "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS,
+            "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS, "kernels": r["kernels"],
+            "spec_recomputed_per_step": r["spec_recomputed_per_step"],
             "ratio_to_headline": r["ms_per_step"] / base["ms_per_step"]}
 
 
@@ -568,6 +573,7 @@ def main():
                        "frames_per_gpu": args.frames, "data_symbols_per_frame": args.data_symbols,
                        "parallelism": f"frames sharded x{world}, no collective (gloo timing only)",
                        "ranks": ranks, "symbols_ok": r7["symbols_ok"], "stage_ms": r7["stage_ms"],
+                       "kernels": r7["kernels"], "spec_recomputed_per_step": r7["spec_recomputed_per_step"],
                        "msym_s_all_symbols": r7["msym_s_all"] * world,
                        "pipeline_gbs_per_gpu": r7["pipeline_gbs"]},
             "roofline": roofline(r7, probe),

@@ -177,7 +177,18 @@ int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls);
 #define LORA_KERNEL_FUSED 8
 #define LORA_KERNEL_GENERIC 16
 #define LORA_KERNEL_FRAME_MAX_WAVE 32 /* with FRAME_MAX: the one-wave-per-frame variant (short frames) */
+#define LORA_KERNEL_SPEC 64 /* the speculative single-read pipeline (with ESTIMATE + DEMOD) */
 int lora_demod_last_kernels(const lora_demod_plan* plan);
+
+/* LEGACY frames at osr 1 without a window, SF 6-12, 3..80 symbols, run as a speculative
+ * single-read pipeline (LORA_KERNEL_SPEC): the offset estimate on unscaled samples, every
+ * data symbol demodulated once while the frame maximum is reduced from the same read, then
+ * the exact estimate, with each data symbol either certified by a rounding bound on its
+ * argmax margin or recomputed exactly - the outputs equal the reference's (LoRaDemod.cpp:
+ * 49-195) either way.  This returns how many data symbols this plan has recomputed so far
+ * (synchronises the device; for tests and diagnostics).  LORA_MI355X_SPEC=0 disables the
+ * pipeline (three launches: frame max, estimate, demod). */
+int64_t lora_demod_spec_recomputed(lora_demod_plan* plan);
 
 /* Thread-local text of the last error ("" if none). */
 const char* lora_last_error(void);

@@ -127,6 +127,13 @@ bool bw_ok(unsigned bw) { return bw == 125000 || bw == 250000 || bw == 500000; }
 size_t ws_counter_bytes(int64_t frames) {  // partial maxima, kMaxBpf per frame
   return ((size_t)frames * lora::kMaxBpf * sizeof(uint32_t) + 255) & ~size_t(255);
 }
+size_t ws_params_bytes(int64_t frames) {  // FrameParams per frame
+  return ((size_t)frames * sizeof(lora::FrameParams) + 255) & ~size_t(255);
+}
+// speculative pipeline: pre-pass FrameParams + one margin per data symbol (<= kMaxBpf - 1)
+size_t ws_spec_bytes(int64_t frames) {
+  return ws_params_bytes(frames) + (((size_t)frames * (lora::kMaxBpf - 1) * sizeof(float) + 255) & ~size_t(255));
+}
 
 // ---------------------------------------------------------------------------------
 // Kernels
@@ -665,6 +672,8 @@ struct lora_demod_plan {
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), results invalid
   int max_chunks;  // 2-stream pipeline depth (LORA_MI355X_CHUNKS, default 1 = off)
   size_t fused_lds_max;  // frame-resident single-read kernel: LDS image limit (0 = off)
+  int spec;              // speculative single-read pipeline enabled (LORA_MI355X_SPEC, default 1)
+  unsigned int* spec_fix = nullptr;  // device counter of symbols the pipeline recomputed
   int last_kernels = 0;  // LORA_KERNEL_* mask of the last lora_demod_batch call
   // Two-stream pipeline: per-frame prep (max + estimate) of chunk c+1 on `aux`
   // overlaps the symbol demod of chunk c on the caller's stream.
@@ -792,7 +801,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   const size_t b_tw = sizeof(cf) * N, b_down = sizeof(cf) * 2 * step, b_down1 = sizeof(cf) * N,
                b_win = sizeof(float) * N, b_rev = sizeof(uint16_t) * N, b_twT = sizeof(cf) * twT.size();
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  const size_t total = al(b_tw) + al(b_down) + al(b_down1) + al(b_win) + al(b_rev) + al(b_twT);
+  const size_t total = al(b_tw) + al(b_down) + al(b_down1) + al(b_win) + al(b_rev) + al(b_twT) + 256;
 
   int prev = 0;
   HIP_TRY(hipGetDevice(&prev));
@@ -822,6 +831,8 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
     // image limit in KiB (80 = two frames per CU), unset or 0 = off.  It is bit-exact but
     // slower than the three launches on the measured workloads:
     // its per-frame estimate chain is serial latency that two frames per CU cannot hide.
+    const char* sp = std::getenv("LORA_MI355X_SPEC");
+    plan->spec = !(sp && sp[0] == '0');
     const char* fu = std::getenv("LORA_MI355X_FUSED");
     const int fk = fu ? std::max(0, std::min(160, std::atoi(fu))) : 0;
     plan->fused_lds_max = fk == 0 ? 0 : (size_t)fk * 1024 - (fk <= 80 ? 256 : 128);
@@ -840,6 +851,8 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   cf* twT_dev = twT.empty() ? nullptr : reinterpret_cast<cf*>(b);
   plan->twTA = twTA_off >= 0 ? twT_dev + twTA_off : nullptr;
   plan->twTB = twTB_off >= 0 ? twT_dev + twTB_off : nullptr;
+  b += al(b_twT);
+  plan->spec_fix = reinterpret_cast<unsigned int*>(b);
   hipError_t e = hipStreamCreateWithFlags(&plan->aux, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->ev_fork, hipEventDisableTiming);
   for (int c = 0; c < kMaxChunks && e == hipSuccess; ++c)
@@ -850,6 +863,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   if (e == hipSuccess) e = hipMemcpy(plan->win, win.data(), b_win, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->rev, rev.data(), b_rev, hipMemcpyHostToDevice);
   if (e == hipSuccess && !twT.empty()) e = hipMemcpy(twT_dev, twT.data(), b_twT, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(plan->spec_fix, 0, sizeof(unsigned int));
   hipSetDevice(prev);
   if (e != hipSuccess) {
     const std::string msg = std::string("plan setup: ") + hipGetErrorString(e);
@@ -928,7 +942,14 @@ int64_t lora_demod_symbols_per_frame(const lora_demod_plan* plan, int64_t frame_
 size_t lora_demod_workspace_bytes(const lora_demod_plan* plan, int64_t frames) {
   (void)plan;
   if (frames <= 0) return 0;
-  return ws_counter_bytes(frames) + (size_t)frames * sizeof(lora::FrameParams);
+  return ws_counter_bytes(frames) + ws_params_bytes(frames) + ws_spec_bytes(frames);
+}
+
+int64_t lora_demod_spec_recomputed(lora_demod_plan* plan) {
+  if (!plan) return set_error(LORA_EINVAL, "null plan");
+  unsigned int v = 0;
+  HIP_TRY(hipMemcpy(&v, plan->spec_fix, sizeof(v), hipMemcpyDeviceToHost));
+  return (int64_t)v;
 }
 
 int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames, int64_t frame_len,
@@ -980,6 +1001,10 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   uint32_t* maxbits = reinterpret_cast<uint32_t*>(wsb);
   a.maxbits = maxbits;
   a.fp = reinterpret_cast<lora::FrameParams*>(wsb + ws_counter_bytes(frames));
+  a.fp_spec = reinterpret_cast<lora::FrameParams*>(wsb + ws_counter_bytes(frames) + ws_params_bytes(frames));
+  a.spec_marg = reinterpret_cast<float*>(wsb + ws_counter_bytes(frames) + 2 * ws_params_bytes(frames));
+  a.spec_max = maxbits;
+  a.spec_fix = plan->spec_fix;
   a.syms = out->symbols;
   a.sym_stride = out->sym_stride;
   a.sync = out->sync;
@@ -1076,7 +1101,43 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
       fused = lora::launch_fused(a, frames, plan->fused_lds_max, st);
     }
     if (fused) kernels |= LORA_KERNEL_FUSED;
-    if (!fused) {
+    // Speculative single-read pipeline (LoRaDemod.cpp:59-192 reordered, results identical):
+    //   1. offset estimate on UNSCALED samples (k_est_fast<SPEC=1>), plus the maximum of the
+    //      samples outside the data-symbol windows it implies;
+    //   2. every data symbol with those offsets on unscaled samples (k_demod_fast<SPEC>),
+    //      which also reduces each window's max(|I|,|Q|) - the frame-max pass's work, from
+    //      the same read - and records the symbol's argmax margin;
+    //   3. the exact estimate from the assembled maximum (k_est_fast<SPEC=2>): outputs, sync
+    //      word, and each speculative symbol either certified (its margin exceeds the
+    //      rounding bound, so the reference's argmax is the same bin) or recomputed exactly.
+    // A frame that needs no rescaling (max <= 1) is exact as computed.  The IQ is read once
+    // plus symbols 0/1 twice; lora_demod_spec_recomputed() counts recomputations.
+    const bool spec_ok = !fused && plan->use_fast && plan->spec && p.mode == LORA_MODE_LEGACY && p.osr == 1 &&
+                         !a.hann && !a.fast_rot && !a.ablate && p.sf >= 6 && total >= 3 &&
+                         total - 2 + 1 <= lora::kMaxBpf;
+    bool spec_done = false;
+    if (spec_ok) {
+      KArgs as = a;
+      as.mx_bpf = (int)(total - 2) + 1;
+      as.maxbits = maxbits;
+      bool ok;
+      {
+        ProfScope ps(plan, 1, st);
+        ok = lora::launch_spec(as, frames, 0, st);
+      }
+      if (ok) {
+        ProfScope ps(plan, 2, st);
+        ok = lora::launch_spec(as, frames, 1, st);
+      }
+      if (ok) {
+        ProfScope ps(plan, 1, st);
+        ok = lora::launch_spec(as, frames, 2, st);
+      }
+      if (!ok) rc = set_error(LORA_EIO, "speculative pipeline launch failed");
+      spec_done = true;
+      kernels |= LORA_KERNEL_SPEC | LORA_KERNEL_ESTIMATE | LORA_KERNEL_DEMOD;
+    }
+    if (!fused && !spec_done) {
       prep(a, maxbits, frames, st);
       demod(a, frames, st);
     }

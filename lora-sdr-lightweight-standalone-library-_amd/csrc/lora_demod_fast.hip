@@ -209,9 +209,14 @@ __device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__
 
 // The other lanes' share of one pass: read R points from LDS, run the stages,
 // either write them back or fold them into the argmax key.
+#ifndef LORA_SPEC_ABL
+#define LORA_SPEC_ABL 0  // A/B only: 1 = skip the speculative extras (results invalid)
+#endif
+
 template <int R, int N, int MA, int SF, int T, int P, bool LAST>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
-                                         uint64_t& key, const cf* __restrict__ twT = nullptr) {
+                                         uint64_t& key, const cf* __restrict__ twT = nullptr,
+                                         float* second = nullptr) {
   constexpr int NG = P / R;
 #pragma unroll
   for (int gg = 0; gg < NG; ++gg) {
@@ -233,7 +238,7 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     // The last pass covers all N bins with cc == 0: bin = (l + T*gg) + MA*u.  Scanning
     // u-major / gg-minor visits the lane's bins in increasing order, so a strict '>'
     // keeps the lowest index among equal maxima (LoRaDetector.hpp:50-57).
-    float best = 0.0f;
+    float best = 0.0f, sec = 0.0f;
     uint32_t bi = (uint32_t)l;
 #pragma unroll
     for (int u = 0; u < R; ++u)
@@ -242,12 +247,16 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
         const cf v = x[gg * R + u];
         const float m2 = v.re * v.re + v.im * v.im;
         const uint32_t bin = (uint32_t)(l + T * gg + MA * u);
+        // runner-up |X|^2 of the lane (an equal value counts: margin 0); sec <= best, so
+        // the median of (sec, m2, best) is best if m2 > best, else max(sec, m2)
+        if (second) sec = __builtin_amdgcn_fmed3f(sec, m2, best);
         if (m2 > best) {
           best = m2;
           bi = bin;
         }
       }
     key = ((uint64_t)__float_as_uint(best) << 32) | (uint32_t)(~bi);
+    if (second) *second = sec;
   }
 }
 
@@ -395,7 +404,7 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
 // argmax key.  KEEP: leave the spectrum in natural order in `row` (padded address
 // paddr(bin)) for the estimate's neighbour bins; NPASS == 1 keeps it in z.
 template <int SF, bool KEEP, int ABL>
-__device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a) {
+__device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
   constexpr bool WL = G::WAVE_LOCAL;
@@ -428,13 +437,13 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
     constexpr int RL = G::NPASS == 2 ? G::RA : G::RB;   // last pass span
     constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row, z, l, a.tw, key, a.twTA);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row, z, l, a.tw, key, a.twTA, second);
     } else {
       pass_lds<G::RA, N, G::MA_A, SF, T, P, false>(row, z, l, a.tw, key, a.twTA);
       block_sync<WL>();
       write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
       block_sync<WL>();
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true>(row, z, l, a.tw, key, a.twTB);
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true>(row, z, l, a.tw, key, a.twTB, second);
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)
@@ -509,6 +518,37 @@ __device__ __forceinline__ uint64_t symbol_key(uint64_t key, int tid, uint64_t* 
   }
 }
 
+// Speculative demod (SPEC): the maxima of `a` and `b` over the symbol's T lanes (every
+// lane gets them).  Wave-local groups use shuffles; T > 64 adds one LDS round through
+// `rf` (2 floats per wave), which must not alias live data.
+template <int SF>
+__device__ __forceinline__ void group_reduce2(float& a, float& b, int tid, float* rf) {
+  constexpr int T = Geo<SF>::T;
+  constexpr int W = T < 64 ? T : 64;
+#pragma unroll
+  for (int o = W >> 1; o > 0; o >>= 1) {
+    a = fmaxf(a, __shfl_xor(a, o, 64));
+    b = fmaxf(b, __shfl_xor(b, o, 64));
+  }
+  if constexpr (T > 64) {
+    const int w = tid >> 6;
+    if ((tid & 63) == 0) {
+      rf[2 * w] = a;
+      rf[2 * w + 1] = b;
+    }
+    __syncthreads();
+    constexpr int WPS = T / 64;
+    const int wb = (w / WPS) * WPS;
+    a = rf[2 * wb];
+    b = rf[2 * wb + 1];
+#pragma unroll
+    for (int q = 1; q < WPS; ++q) {
+      a = fmaxf(a, rf[2 * (wb + q)]);
+      b = fmaxf(b, rf[2 * (wb + q) + 1]);
+    }
+  }
+}
+
 // MODE 0: LEGACY + fused dechirp, osr 1, no window (the benchmark configuration);
 // MODE 1: LEGACY on already-dechirped input, osr 1, no window (lora_demodulate's own
 //         contract); MODE 2: every other LEGACY / API configuration, flags read at run
@@ -526,7 +566,12 @@ constexpr int demod_waves_per_eu() {
   return SF >= 6 ? 4 : 1;
 }
 
-template <int SF, int MODE, int ABL = 0, bool FAST = false>
+// SPEC: the speculative single-read pipeline's symbol pass (lora_capi.hip): the pre-pass
+// offsets (fp_spec) on unscaled samples, and per data symbol its window's partial
+// max(|I|,|Q|) (spec_max, slot s - s0 of the frame) and the margin |X1| - |X2| between
+// the top bin and the runner-up (spec_marg), which k_est_fast<SPEC = 2> uses to certify
+// or recompute the symbol.
+template <int SF, int MODE, int ABL = 0, bool FAST = false, bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   using G = Geo<SF>;
@@ -551,7 +596,7 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   const int64_t wc = valid ? w : work - 1;  // clamp: invalid lanes mirror a valid symbol
   const int64_t f = wc / per;
   const int s = s0 + (int)(wc - f * per);
-  const FrameParams p = RAW ? FrameParams{0.0f, 0.0f, 0.0f, 1.0f, 0, 0, 0, 0} : a.fp[f];
+  const FrameParams p = RAW ? FrameParams{0.0f, 0.0f, 0.0f, 1.0f, 0, 0, 0, 0} : (SPEC ? a.fp_spec[f] : a.fp[f]);
   int64_t base;
   int cg;
   sym_base(s, step, a.frame_len, p.t_off, base, cg);
@@ -562,10 +607,31 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
 
   cf in[P], z[P];
   gather_points<SF, ABL>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, scale, in);
+  float pm = 0.0f;
+  if constexpr (SPEC && !LORA_SPEC_ABL) {  // the window's dechirped, unscaled samples (scale is 1 here)
+    // max(pm, |re|, |im|) in one instruction per point (fmaxf would canonicalize each
+    // operand first); pinned here, as the samples arrive: left to itself the compiler
+    // sinks it to its only use after the FFT and keeps all 2P inputs live (spills).
+#pragma unroll
+    for (int q = 0; q < P; ++q) asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(pm) : "v"(in[q].re), "v"(in[q].im));
+  }
   rotate_place<SF, !RAW, ABL, FAST>(in, z, start, p.rate, hann, a.win, l);
-  uint64_t key = fft_key<SF, false, ABL>(z, rows + (size_t)g * rowc, l, a);
-  key = symbol_key<SF>(key, tid, red);
+  if constexpr (SPEC && !LORA_SPEC_ABL) asm volatile("" : "+v"(pm));
+  float sec = 0.0f;
+  const uint64_t lkey =
+      fft_key<SF, false, ABL>(z, rows + (size_t)g * rowc, l, a, SPEC && !LORA_SPEC_ABL ? &sec : nullptr);
+  const uint64_t key = symbol_key<SF>(lkey, tid, red);
   if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + (s - s0)] = (uint16_t)key_index(key);
+  if constexpr (SPEC && !LORA_SPEC_ABL) {
+    // runner-up over the symbol: the top lane offers its own runner-up, the others their best
+    float r2 = lkey == key ? sec : key_value(lkey);
+    group_reduce2<SF>(r2, pm, tid, reinterpret_cast<float*>(smem + 64));
+    if (l == 0 && valid) {
+      const int64_t per = a.total - s0;
+      a.spec_marg[f * per + (s - s0)] = sqrtf(key_value(key)) - sqrtf(r2);
+      a.spec_max[f * a.mx_bpf + (s - s0)] = __float_as_uint(pm);
+    }
+  }
 }
 
 // Offset estimate + sync symbols, one T-lane group per frame (LoRaDemod.cpp:79-135,
@@ -590,16 +656,27 @@ struct EstGeo {
   static constexpr bool PAIR = LORA_EST_PAIR && SF >= 7 && Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2;
 };
 
-template <int SF, int MODE>
+// SPEC (the speculative single-read pipeline, LEGACY osr-1 unwindowed frames, see
+// lora_capi.hip): 0 = the estimate as above; 1 = pre-pass: the estimate on UNSCALED
+// samples into fp_spec plus the maximum of the samples no data-symbol window covers
+// (symbols 0/1 and the frame tail, one partial slot), and unless that maximum already
+// exceeds 1, the sync word (fp_spec pad0; no outputs); 2 = with the maximum assembled from the demod's window partials: a frame
+// that is not rescaled takes the pre-pass results as they are; any other gets the exact
+// estimate, its outputs and sync word, then the certification of every data symbol the
+// demod computed from unscaled samples with the pre-pass offsets: a symbol whose argmax
+// margin exceeds the rounding bound keeps its index, any other is recomputed exactly here.
+template <int SF, int MODE, int SPEC = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
   constexpr int SPB = (T >= 64 ? 256 : 64) / T;  // frames per block (block = max(T, 64))
   constexpr bool DYN = MODE == 2;
+  static_assert(SPEC == 0 || !DYN, "the speculative pipeline covers MODE 0/1 only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint64_t red[4];
   __shared__ FrameParams sp[SPB];
+  __shared__ unsigned long long fmask[SPEC == 2 ? SPB : 1][2];
   const int tid = threadIdx.x;
   const int step = DYN ? a.step : N;
   const int osr = DYN ? a.osr : 1;
@@ -613,9 +690,32 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   const int64_t f = valid ? f0 : frames - 1;
   const cf* __restrict__ x = a.iq + f * a.frame_stride;
   cf* row = reinterpret_cast<cf*>(smem) + (size_t)g * rowc;
-  const float maxv = legacy ? frame_maxv(a, f) : 0.0f;
+  // LoRaDemod.cpp:59-67 max_amp from the frame's partials: the group's lanes load them
+  // in parallel (up to kMaxBpf, one dependent load chain per lane is latency-bound)
+  float maxv = 0.0f;
+  if (legacy && SPEC != 1) {
+    for (int c = l; c < a.mx_bpf; c += T) maxv = fmaxf(maxv, __uint_as_float(a.maxbits[f * a.mx_bpf + c]));
+    maxv = __uint_as_float((uint32_t)(symbol_key<SF>((uint64_t)__float_as_uint(maxv) << 32, tid, red) >> 32));
+  }
   const int scaled = maxv > 1.0f;
   const float scale = scaled ? 1.0f / maxv : 1.0f;
+  if constexpr (SPEC == 2) {
+    // max <= 1: no rescaling, so the pre-pass estimate, its sync word and every
+    // speculative symbol are already the reference's (identical inputs and arithmetic).
+    // Frame-uniform exit: T-lane groups are whole waves or lie within one, and waves that
+    // have ended drop out of the other frames' later s_barriers.
+    if (!scaled) {
+      if (l == 0 && valid) {
+        const FrameParams qs = a.fp_spec[f];
+        a.fp[f] = qs;
+        if (a.cfo) a.cfo[f] = qs.cfo;
+        if (a.toff) a.toff[f] = qs.toff;
+        if (a.max_amp) a.max_amp[f] = maxv;
+        if (a.sync) a.sync[f] = (uint8_t)qs.pad0;
+      }
+      return;
+    }
+  }
 
   float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
   bool have_prev = false;
@@ -750,14 +850,46 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     q.pad0 = q.pad1 = 0;
     sp[g] = q;
     if (valid) {
-      a.fp[f] = q;
-      if (a.cfo) a.cfo[f] = cfo;
-      if (a.toff) a.toff[f] = toff;
-      if (a.max_amp) a.max_amp[f] = maxv;
+      if constexpr (SPEC == 1) {
+        a.fp_spec[f] = q;
+      } else {
+        a.fp[f] = q;
+        if (a.cfo) a.cfo[f] = cfo;
+        if (a.toff) a.toff[f] = toff;
+        if (a.max_amp) a.max_amp[f] = maxv;
+      }
     }
   }
   block_sync<G::WAVE_LOCAL>();
   const FrameParams q = sp[g];
+  if constexpr (SPEC == 1) {
+    // The samples outside every data-symbol window of the pre-pass offsets: [0, start of
+    // symbol 2's window) and [end of the last window, frame_len).  With the windows'
+    // partial maxima (k_demod_fast<SPEC>) they make up the whole frame's maximum.
+    const int per = a.total - 2;
+    int64_t b2, bl;
+    int cg;
+    sym_base(2, step, a.frame_len, q.t_off, b2, cg);
+    sym_base(a.total - 1, step, a.frame_len, q.t_off, bl, cg);
+    const int64_t xend = bl + step;
+    float m = 0.0f;
+    for (int64_t j = l; j < b2; j += T) {
+      cf v = x[j];
+      if (dech) v = cmul(v, a.down[j % step]);
+      m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+    }
+    for (int64_t j = xend + l; j < a.frame_len; j += T) {
+      cf v = x[j];
+      if (dech) v = cmul(v, a.down[j % step]);
+      m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+    }
+    const uint64_t mk = symbol_key<SF>((uint64_t)__float_as_uint(m) << 32, tid, red);
+    if (l == 0 && valid) a.spec_max[f * a.mx_bpf + per] = (uint32_t)(mk >> 32);
+    // Already above 1: the frame is rescaled, so k_est_fast<SPEC = 2> recomputes the
+    // estimate and the sync word; skip them here (frame-uniform exit).
+    if (__uint_as_float((uint32_t)(mk >> 32)) > 1.0f) return;
+    block_sync<G::WAVE_LOCAL>();  // red is reused by the sync symbols
+  }
   uint32_t sw[2];
   if constexpr (PAIR) {
     cf* row1 = row + (size_t)EstGeo<SF>::SPB * rowc;
@@ -791,9 +923,71 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     sw[s] = key_index(key);
     block_sync<G::WAVE_LOCAL>();
   }
-  if (l == 0 && valid && a.sync) {
+  if (l == 0 && valid) {
     const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
-    a.sync[f] = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
+    const uint8_t word = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
+    if constexpr (SPEC == 1) {
+      a.fp_spec[f].pad0 = word;  // the pre-pass sync word, final when the frame is not rescaled
+    } else if (a.sync) {
+      a.sync[f] = word;
+    }
+  }
+  if constexpr (SPEC == 1) return;
+  if constexpr (SPEC == 2) {
+    // ---- certification of the data symbols the demod computed speculatively ----
+    // The demod used the pre-pass offsets qs on unscaled samples y; the reference uses q
+    // on y * scale.  In exact arithmetic the two spectra differ by the factor `scale` and
+    // the rotation difference; every fp32 rounding of the chain (the product y * scale,
+    // the phase start + rate * i, sincosf, the rotation product, kissfft's butterflies,
+    // |X|^2) perturbs a bin by at most E * sum_i |y_i| with E = (8 log2 N + 32) * 2^-24
+    // (the FFT's per-stage error is bounded by its partial sums <= sum_i |y_i|), and a
+    // phase difference d(phi) by at most d(phi) * sum_i |y_i|.  So if the speculative
+    // top bin exceeds the runner-up by more than twice the bound (times 2 for safety),
+    // the reference's argmax is the same bin, strictly (no tie).  Otherwise - or when the
+    // two estimates disagree on t_off - the symbol is recomputed exactly below.
+    const FrameParams qs = a.fp_spec[f];
+    const int per = a.total - 2;
+    const bool same_t = qs.t_off == q.t_off;
+    if (l < 2) fmask[g][l] = 0;
+    block_sync<G::WAVE_LOCAL>();
+    {  // rescaled frames only (the others left above)
+      const double eps = 1.0 / 16777216.0;
+      const double E = (8.0 * SF + 32.0) * eps;
+      const double drate = fabs((double)q.rate - (double)qs.rate);
+      const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
+      const double tabs = (double)abs(q.t_off);
+      for (int j = l; j < per; j += T) {
+        const float d = a.spec_marg[f * per + j];
+        // sum_i |y_i| <= sum_i (|re_i| + |im_i|) <= 2 N max(|re|, |im|) over the window
+        const double n1 = 2.0 * N * (double)__uint_as_float(a.spec_max[f * a.mx_bpf + j]);
+        const double L = (double)(2 + j) * N + tabs + N;  // |phase argument| scale of symbol 2+j
+        const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E);
+        const bool ok = same_t && (double)d > 4.0 * B;
+        if (!ok) atomicOr(&fmask[g][j >> 6], 1ull << (j & 63));
+      }
+    }
+    block_sync<G::WAVE_LOCAL>();
+    const unsigned long long fm0 = fmask[g][0], fm1 = fmask[g][1];
+    if (fm0 | fm1) {
+      cf in[P], z[P];
+      for (int j = 0; j < per; ++j) {
+        if (!(((j < 64) ? fm0 >> j : fm1 >> (j - 64)) & 1)) continue;  // group-uniform
+        const int s = 2 + j;
+        int64_t base;
+        int cg;
+        sym_base(s, step, a.frame_len, q.t_off, base, cg);
+        const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
+        gather_points<SF, 0>(a, x + base, l, osr, step, cg, 1, dech, q.scaled ? q.scale : 1.0f, in);
+        rotate_place<SF, true, 0>(in, z, start, q.rate, hann, a.win, l);
+        uint64_t key = fft_key<SF, false, 0>(z, row, l, a);
+        key = symbol_key<SF>(key, tid, red);
+        if (l == 0 && valid) {
+          if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)key_index(key);
+          atomicAdd(a.spec_fix, 1u);
+        }
+        block_sync<G::WAVE_LOCAL>();  // row is rewritten by the next transform
+      }
+    }
   }
 }
 
@@ -1160,7 +1354,7 @@ int row_complex() {
   return lds_row<SF>();
 }
 
-template <int SF, int MODE>
+template <int SF, int MODE, int SPEC = 0>
 bool launch_est_mode(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
   constexpr int T = G::T;
@@ -1170,11 +1364,11 @@ bool launch_est_mode(const KArgs& a, int64_t frames, hipStream_t st) {
   const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * (size_t)SPB * rowc * (EstGeo<SF>::PAIR && MODE <= 1 ? 2 : 1);
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_est_fast<SF, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)k_est_fast<SF, MODE, SPEC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
       return false;
   const int64_t grid = (frames + SPB - 1) / SPB;
-  hipLaunchKernelGGL((k_est_fast<SF, MODE>), dim3((unsigned)grid), dim3(BLOCK), lds, st, a, frames, rowc);
+  hipLaunchKernelGGL((k_est_fast<SF, MODE, SPEC>), dim3((unsigned)grid), dim3(BLOCK), lds, st, a, frames, rowc);
   return true;
 }
 
@@ -1186,20 +1380,35 @@ bool launch_est_sf(const KArgs& a, int64_t frames, hipStream_t st) {
   return launch_est_mode<SF, 2>(a, frames, st);
 }
 
-template <int SF, int MODE, int ABL = 0, bool FAST = false>
+template <int SF, int MODE, int ABL = 0, bool FAST = false, bool SPEC = false>
 bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
   const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * (size_t)G::SPW * rowc;
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_demod_fast<SF, MODE, ABL, FAST>,
+    if (hipFuncSetAttribute((const void*)k_demod_fast<SF, MODE, ABL, FAST, SPEC>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return false;
   const int64_t grid = (work + G::SPW - 1) / G::SPW;
-  hipLaunchKernelGGL((k_demod_fast<SF, MODE, ABL, FAST>), dim3((unsigned)grid), dim3(256), lds, st, a, s0, work,
-                     rowc);
+  hipLaunchKernelGGL((k_demod_fast<SF, MODE, ABL, FAST, SPEC>), dim3((unsigned)grid), dim3(256), lds, st, a, s0,
+                     work, rowc);
   return true;
+}
+
+// The speculative pipeline's three launches for SF 6-12, MODE 0/1 (see lora_capi.hip).
+template <int SF>
+bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
+  if constexpr (SF < 6) {
+    return false;
+  } else {
+    const int64_t work = frames * (int64_t)(a.total - 2);
+    if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
+    if (stage == 1)
+      return a.dechirp ? launch_mode<SF, 0, 0, false, true>(a, 2, work, st)
+                       : launch_mode<SF, 1, 0, false, true>(a, 2, work, st);
+    return a.dechirp ? launch_est_mode<SF, 0, 2>(a, frames, st) : launch_est_mode<SF, 1, 2>(a, frames, st);
+  }
 }
 
 template <int SF>
@@ -1253,6 +1462,19 @@ bool launch_fused(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st
     case 6: return launch_fused_sf<6>(a, frames, lds_max, st);
     case 7: return launch_fused_sf<7>(a, frames, lds_max, st);
     case 8: return launch_fused_sf<8>(a, frames, lds_max, st);
+    default: return false;
+  }
+}
+
+bool launch_spec(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
+  switch (a.sf) {
+    case 6: return launch_spec_sf<6>(a, frames, stage, st);
+    case 7: return launch_spec_sf<7>(a, frames, stage, st);
+    case 8: return launch_spec_sf<8>(a, frames, stage, st);
+    case 9: return launch_spec_sf<9>(a, frames, stage, st);
+    case 10: return launch_spec_sf<10>(a, frames, stage, st);
+    case 11: return launch_spec_sf<11>(a, frames, stage, st);
+    case 12: return launch_spec_sf<12>(a, frames, stage, st);
     default: return false;
   }
 }

@@ -34,6 +34,13 @@ struct KArgs {
   int fast_rot;  // LORA_PRECISION_FAST: hardware sin/cos rotation in the symbol demod
   const cf* twTA;  // fast kernels: slot-major twiddles of LDS pass A / B (or null)
   const cf* twTB;
+  // Speculative single-read pipeline (lora_demod_batch, LEGACY osr-1 unwindowed frames):
+  // the estimate on unscaled samples, the data symbols' window maxima and certification
+  // margins written by the symbol demod, and a device counter of exact recomputations.
+  FrameParams* fp_spec = nullptr;  // [frame] estimate on unscaled samples
+  float* spec_marg = nullptr;      // [frame][data symbol]: |X1| - |X2| of the speculative spectrum
+  uint32_t* spec_max = nullptr;    // writable alias of maxbits
+  unsigned int* spec_fix = nullptr;
 };
 
 // Shape of the fast kernels' LDS passes for SF >= 6 (lora_demod_fast.hip Geo<SF>): pass-1
@@ -79,6 +86,13 @@ bool launch_demod_fast(const KArgs& a, int s0, int64_t work, hipStream_t st);
 // frame staged in LDS) for LEGACY osr-1 unwindowed frames of SF 6-8 whose LDS image is at
 // most lds_max bytes; false = not covered (caller runs the three-launch path).
 bool launch_fused(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st);
+
+// Speculative single-read pipeline, SF 6-12, LEGACY osr-1 unwindowed frames with >= 3
+// symbols (lora_capi.hip): stage 0 = k_est_fast<SPEC=1> (estimate on unscaled samples +
+// the maximum outside the data windows), 1 = k_demod_fast<SPEC> (every data symbol, window
+// maxima and certification margins), 2 = k_est_fast<SPEC=2> (exact estimate, outputs,
+// sync word, certification and exact recomputation).  a.mx_bpf = data symbols + 1.
+bool launch_spec(const KArgs& a, int64_t frames, int stage, hipStream_t st);
 
 // Offset estimate + sync symbols with the same FFT machinery, one lane group per frame
 // (frames with >= 2 whole symbols; false = not covered, use k_estimate).

@@ -26,7 +26,8 @@ LORA_MODE_API = 1
 LORA_MODE_RAW = 2
 
 # lora_demod_last_kernels bits
-KERNEL_BITS = {"frame_max": 1, "estimate": 2, "demod": 4, "fused": 8, "generic": 16, "frame_max_wave": 32}
+KERNEL_BITS = {"frame_max": 1, "estimate": 2, "demod": 4, "fused": 8, "generic": 16, "frame_max_wave": 32,
+               "spec": 64}
 
 # Every symbol include/lora_mi355x.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (
@@ -41,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "lora_demod_profile_enable",
     "lora_demod_profile_read",
     "lora_demod_last_kernels",
+    "lora_demod_spec_recomputed",
     "lora_last_error",
     "lora_version",
 )
@@ -118,6 +120,8 @@ def lib() -> C.CDLL:
     L.lora_demod_profile_read.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int)]
     L.lora_demod_last_kernels.restype = C.c_int
     L.lora_demod_last_kernels.argtypes = [C.c_void_p]
+    L.lora_demod_spec_recomputed.restype = C.c_int64
+    L.lora_demod_spec_recomputed.argtypes = [C.c_void_p]
     L.lora_last_error.restype = C.c_char_p
     L.lora_version.restype = C.c_char_p
     _lib = L

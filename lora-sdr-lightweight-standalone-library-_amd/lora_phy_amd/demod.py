@@ -116,10 +116,16 @@ class DemodPlan:
         return _capi.check(self._lib.lora_demod_symbols_per_frame(self._h, int(frame_len)))
 
     def last_kernels(self) -> set:
-        """Kernels the last run() launched: {"fused"} for the frame-resident single-read
-        path, {"frame_max", "estimate", "demod"} for the three-launch path (+"generic")."""
+        """Kernels the last run() launched: {"spec", "estimate", "demod"} for the speculative
+        single-read pipeline, {"frame_max", "estimate", "demod"} for the three-launch path
+        (+"generic", "frame_max_wave"), {"fused"} for the opt-in frame-resident kernel."""
         m = self._lib.lora_demod_last_kernels(self._h)
         return {k for k, b in _capi.KERNEL_BITS.items() if m & b}
+
+    def spec_recomputed(self) -> int:
+        """Data symbols the speculative pipeline has recomputed exactly on this plan (their
+        certification margin was too small); synchronises the device."""
+        return _capi.check(self._lib.lora_demod_spec_recomputed(self._h))
 
     def _workspace(self, frames: int) -> torch.Tensor:
         need = self._lib.lora_demod_workspace_bytes(self._h, int(frames))

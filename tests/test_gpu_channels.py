@@ -3,8 +3,9 @@ per GPU): 1,000,000 SF7 frames of 2 + 16 symbols resident in HBM (18.4 GB), demo
 <= 8 GB chunks like bench.py's channels line, with AWGN from noiseless to 0 dB so frames
 rescale and shift their windows (t_off != 0).  From EVERY chunk, its first and last frames
 and a seeded random sample are checked against the CPU oracle bit for bit (symbols, sync,
-cfo / time_offset bits).  The frame max runs as k_frame_max_wave (frames shorter than two
-4096-sample batches), the path this shape exercises.
+cfo / time_offset bits), through the default speculative single-read pipeline and through
+the three-launch path, whose frame max runs as k_frame_max_wave (frames shorter than two
+4096-sample batches).
 """
 import numpy as np
 import pytest
@@ -17,9 +18,13 @@ def bits(x):
     return np.asarray(x, np.float32).view(np.uint32)
 
 
-def test_configs4_shape_every_chunk_vs_oracle():
+@pytest.mark.parametrize("path", ["spec", "split"])
+def test_configs4_shape_every_chunk_vs_oracle(path):
+    """path "spec": the default speculative single-read pipeline; "split": three launches
+    (LORA_MI355X_SPEC=0) with the one-wave-per-frame max pass."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
+    import os
     import lora_phy_amd as amd
     from oracle.pyoracle import Oracle
 
@@ -41,7 +46,13 @@ def test_configs4_shape_every_chunk_vs_oracle():
         x += torch.view_as_complex(torch.randn((n, L, 2), generator=gn, device=dev)) * sig
         iq[r0:r0 + n] = x
         del x
-    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=dev)
+    if path == "split":
+        os.environ["LORA_MI355X_SPEC"] = "0"
+    try:
+        plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=dev)
+    finally:
+        os.environ.pop("LORA_MI355X_SPEC", None)
+    want = {"spec", "estimate", "demod"} if path == "spec" else {"frame_max", "frame_max_wave", "estimate", "demod"}
     per_chunk = int(8e9 // (L * 8))
     chunks = [(c0, min(per_chunk, frames - c0)) for c0 in range(0, frames, per_chunk)]
     assert len(chunks) == 3
@@ -50,7 +61,7 @@ def test_configs4_shape_every_chunk_vs_oracle():
     for c0, n in chunks:
         res = plan.run(iq[c0:c0 + n])
         torch.cuda.synchronize()
-        assert plan.last_kernels() >= {"frame_max", "frame_max_wave", "estimate", "demod"}, plan.last_kernels()
+        assert plan.last_kernels() == want, plan.last_kernels()
         pick = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 46)]))
         idx = torch.from_numpy(pick).to(dev)
         x = iq[c0:c0 + n].index_select(0, idx).cpu().numpy()

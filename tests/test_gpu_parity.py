@@ -85,11 +85,12 @@ CASES = [  # (sf, osr, hann, dechirp, F, symbols-per-frame, extra samples, kind)
 
 
 def make_plan(amd, path, *args, **kw):
-    """path "fast": register-blocked kernels (LDS passes read slot-major twiddle copies),
-    with the frame-resident single-read kernel wherever it covers the configuration;
-    "split": the same without the frame-resident kernel (three launches,
-    LORA_MI355X_FUSED=0); "gather": the fast kernels gathering twiddles from the natural
-    table (LORA_MI355X_TWT=0); "generic": LDS reference kernel (A/B)."""
+    """path "fast": the default - register-blocked kernels (LDS passes read slot-major
+    twiddle copies), as the speculative single-read pipeline wherever it covers the
+    configuration (LEGACY, osr 1, no window, SF >= 6, >= 3 symbols); "split": the same
+    kernels as three launches (frame max, estimate, demod: LORA_MI355X_SPEC=0);
+    "gather": the fast kernels gathering twiddles from the natural table
+    (LORA_MI355X_TWT=0); "generic": LDS reference kernel (A/B)."""
     import os
 
     if path == "generic":
@@ -97,13 +98,13 @@ def make_plan(amd, path, *args, **kw):
     if path == "gather":
         os.environ["LORA_MI355X_TWT"] = "0"
     if path == "split":
-        os.environ["LORA_MI355X_FUSED"] = "0"
+        os.environ["LORA_MI355X_SPEC"] = "0"
     try:
         return amd.DemodPlan(*args, **kw)
     finally:
         os.environ.pop("LORA_MI355X_GENERIC", None)
         os.environ.pop("LORA_MI355X_TWT", None)
-        os.environ.pop("LORA_MI355X_FUSED", None)
+        os.environ.pop("LORA_MI355X_SPEC", None)
 
 
 @pytest.mark.parametrize("path", ["fast", "split", "gather", "generic"])

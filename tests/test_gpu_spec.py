@@ -1,0 +1,226 @@
+"""GPU: the speculative single-read pipeline (LORA_MI355X_SPEC, default on) is exact.
+
+The pipeline (lora_capi.hip) demodulates every data symbol with offsets
+estimated on the UNSCALED frame, then certifies each symbol against the exact
+(LoRaDemod.cpp:59-67 rescaled) estimate through a rounding-error bound on its
+top-bin / runner-up margin and recomputes the symbols it cannot certify.  These tests
+drive the three outcomes against the CPU oracle, bit for bit:
+
+  * verbatim frames (max(|I|,|Q|) <= 1: no rescaling, nothing to certify),
+  * certified frames (max > 1, margins far above the bound),
+  * recomputed symbols (exact ties between two bins, a tie in the sync pair that moves
+    the time offset, low SNR), which lora_demod_spec_recomputed() counts,
+
+over SF 6-12, plus the eligibility boundary (3 symbols, kMaxBpf) and the three-launch
+path the pipeline replaces.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+SPEC = {"spec", "estimate", "demod"}
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle.pyoracle import Oracle
+
+    return Oracle()
+
+
+@pytest.fixture(scope="module")
+def amd():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import lora_phy_amd
+
+    return lora_phy_amd
+
+
+def bits(x):
+    return np.asarray(x, np.float32).view(np.uint32)
+
+
+def check(O, amd, iq, sf, spec=True):
+    """Run `iq` ([F, L] dechirped frames) through a fresh plan and compare every output
+    with the oracle; returns (plan, recomputed symbols)."""
+    import os
+
+    if not spec:
+        os.environ["LORA_MI355X_SPEC"] = "0"
+    try:
+        plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=False)
+    finally:
+        os.environ.pop("LORA_MI355X_SPEC", None)
+    res = plan.run(torch.from_numpy(np.ascontiguousarray(iq)).cuda())
+    torch.cuda.synchronize()
+    syms = res.symbols.cpu().numpy()
+    sync = res.sync.cpu().numpy()
+    cfo = res.cfo.cpu().numpy()
+    toff = res.time_offset.cpu().numpy()
+    for f in range(iq.shape[0]):
+        osym, osync, ocfo, otoff = O.lora_demodulate(iq[f], sf, 1, False)
+        assert syms.shape[1] == len(osym)
+        np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f} symbols")
+        assert sync[f] == osync, f"frame {f} sync"
+        assert bits(cfo[f]) == bits(ocfo), f"frame {f} cfo {cfo[f]} vs {ocfo}"
+        assert bits(toff[f]) == bits(otoff), f"frame {f} toff {toff[f]} vs {otoff}"
+    return plan, plan.spec_recomputed()
+
+
+def tone(N, k, amp=1.0, ph=0.0):
+    n = np.arange(N)
+    return (amp * np.exp(1j * (2 * np.pi * k * n / N + ph))).astype(np.complex64)
+
+
+def modulated(O, rng, sf, S, F, amp=1.0, noise=0.0):
+    """F dechirped frames of S symbols (2 sync + S-2 data) at amplitude `amp` plus complex
+    Gaussian noise of standard deviation `noise` per component."""
+    N = 1 << sf
+    out = np.zeros((F, S * N), np.complex64)
+    for f in range(F):
+        syms = rng.integers(0, N, S - 2).astype(np.uint16)
+        x = O.dechirp(O.lora_modulate(syms, sf, 1, 125000, amp, int(rng.integers(0, 256))), sf, 1)[: S * N]
+        if noise > 0:
+            x = x + noise * (rng.standard_normal(S * N) + 1j * rng.standard_normal(S * N))
+        out[f] = x.astype(np.complex64)
+    return out
+
+
+@pytest.mark.parametrize("sf", [6, 7, 8, 9, 10, 11, 12])
+def test_verbatim_frames_need_no_recomputation(O, amd, sf):
+    """max(|I|,|Q|) <= 1: the scale is 1, the pre-pass estimate IS the exact one."""
+    rng = np.random.default_rng(100 + sf)
+    iq = modulated(O, rng, sf, 8 if sf < 11 else 5, 6, amp=0.5, noise=0.05)
+    assert np.abs(iq.view(np.float32)).max() <= 1.0
+    plan, fixed = check(O, amd, iq, sf)
+    assert plan.last_kernels() == SPEC
+    assert fixed == 0
+
+
+@pytest.mark.parametrize("sf", [6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("snr_db", [20, 0, -10, -15])
+def test_rescaled_frames_match_oracle(O, amd, sf, snr_db):
+    """max > 1 (rescaled) at high and low SNR: certified or recomputed, always exact."""
+    rng = np.random.default_rng(1000 * sf + snr_db + 50)
+    amp = 2.5
+    noise = amp * 10 ** (-snr_db / 20) / np.sqrt(2)
+    iq = modulated(O, rng, sf, 10 if sf < 11 else 5, 8 if sf < 10 else 3, amp=amp, noise=noise)
+    assert np.abs(iq.view(np.float32)).max() > 1.0
+    plan, fixed = check(O, amd, iq, sf)
+    assert plan.last_kernels() == SPEC
+    assert fixed >= 0
+
+
+@pytest.mark.parametrize("sf", [6, 7, 9, 12])
+def test_equal_power_tie_is_recomputed(O, amd, sf):
+    """Two data-symbol bins of exactly equal power (equal_power_bin_test.cpp's case in the
+    dechirped domain): the margin is ~0, no bound certifies it, the symbol is recomputed
+    exactly and the lowest index wins as in the reference.  The sync pair is bin 0 in
+    phase, so the estimate is (close to) no rotation and the two bins stay equal."""
+    N = 1 << sf
+    S, F = 6, 4
+    iq = np.zeros((F, S * N), np.complex64)
+    for f in range(F):
+        iq[f, :N] = tone(N, 0, 1.7)
+        iq[f, N:2 * N] = tone(N, 0, 1.7)
+        for s in range(2, S):
+            a, b = (5 * s + f) % N, (N // 2 + 7 * s + f) % N
+            iq[f, s * N:(s + 1) * N] = tone(N, a, 1.3) + tone(N, b, 1.3, 0.7)
+    plan, fixed = check(O, amd, iq, sf)
+    assert plan.last_kernels() == SPEC
+    assert fixed > 0
+
+
+def test_sync_pair_tie_moves_time_offset(O, amd):
+    """Equal-power bins in symbol 0 (the time-offset estimate's input) at max > 1: the
+    scaled and unscaled estimates may pick different t_off, which sends the whole frame to
+    exact recomputation; every frame still matches the oracle."""
+    sf, N, S, F = 7, 128, 8, 16
+    rng = np.random.default_rng(9)
+    iq = np.zeros((F, S * N), np.complex64)
+    for f in range(F):
+        iq[f, :N] = tone(N, 10 + f, 1.1) + tone(N, 40 + 3 * f, 1.1, 0.3 * f)
+        iq[f, N:2 * N] = tone(N, 20 + f, 1.4)
+        for s in range(2, S):
+            iq[f, s * N:(s + 1) * N] = tone(N, int(rng.integers(0, N)), 1.2)
+        iq[f] += (0.01 * (rng.standard_normal(S * N) + 1j * rng.standard_normal(S * N))).astype(np.complex64)
+    check(O, amd, iq, sf)
+
+
+@pytest.mark.parametrize("amp", [0.0, 1.0, 1.0000001, 3e4, 1e-30])
+def test_amplitude_extremes(O, amd, amp):
+    """Zero frames (max 0), max exactly 1 and one ulp above, huge and tiny amplitudes."""
+    rng = np.random.default_rng(int(amp * 7) % 1000 + 3)
+    sf = 7
+    iq = modulated(O, rng, sf, 6, 4, amp=1.0)
+    m = np.abs(iq.view(np.float32)).max()
+    iq = (iq * np.float32(amp / m)).astype(np.complex64) if amp > 0 else np.zeros_like(iq)
+    plan, _ = check(O, amd, iq, sf)
+    assert plan.last_kernels() == SPEC
+
+
+@pytest.mark.parametrize("sf,nsym,spec", [(7, 2, False), (7, 3, True), (9, 81, True), (9, 82, False),
+                                          (12, 3, True), (6, 40, True)])
+def test_eligibility_boundary(O, amd, sf, nsym, spec):
+    """The pipeline covers frames of 3 .. kMaxBpf + 1 symbols; others take the three-launch
+    path; both are exact."""
+    rng = np.random.default_rng(sf * 100 + nsym)
+    iq = modulated(O, rng, sf, nsym, 2, amp=1.8, noise=0.3)
+    plan, _ = check(O, amd, iq, sf)
+    assert ("spec" in plan.last_kernels()) == spec
+    if not spec:
+        assert "frame_max" in plan.last_kernels() or "frame_max_wave" in plan.last_kernels()
+
+
+@pytest.mark.parametrize("sf", [7, 12])
+def test_three_launch_path_agrees(O, amd, sf):
+    """LORA_MI355X_SPEC=0 (frame max, estimate, demod) on the same rescaled low-SNR frames."""
+    rng = np.random.default_rng(sf + 31)
+    iq = modulated(O, rng, sf, 8 if sf < 12 else 5, 4, amp=2.0, noise=2.0)
+    plan, fixed = check(O, amd, iq, sf, spec=False)
+    assert "spec" not in plan.last_kernels()
+    assert fixed == 0
+
+
+@pytest.mark.parametrize("sf", [6, 8, 10, 11, 12])
+def test_mixed_frames_in_one_block(O, amd, sf):
+    """Rescaled and unscaled frames side by side (one block holds 256 / T frames; SF11 two
+    frames of two waves each): the unscaled frames leave the estimate kernels early, the
+    others continue through the block's barriers."""
+    rng = np.random.default_rng(300 + sf)
+    F = 8 if sf < 11 else 4
+    iq = modulated(O, rng, sf, 5, F, amp=0.6, noise=0.02)
+    iq[1::2] *= np.float32(4.0)
+    if F > 2:
+        iq[2, 7] = np.complex64(1.5 + 0.0j)  # rescaled by a single sample in symbol 0
+    plan, _ = check(O, amd, iq, sf)
+    assert plan.last_kernels() == SPEC
+
+
+def test_ragged_tail_and_many_frames(O, amd):
+    """Frame length not a symbol multiple (the tail is ignored) over 700 frames (many lane
+    groups per launch), mixed amplitudes."""
+    sf, N = 8, 256
+    rng = np.random.default_rng(17)
+    F = 700
+    base = modulated(O, rng, sf, 5, 8, amp=1.0, noise=0.2)
+    iq = np.concatenate([base[rng.integers(0, 8, F)], np.zeros((F, 37), np.complex64)], axis=1)
+    iq *= rng.choice([0.3, 1.0, 2.0, 50.0], F).astype(np.float32)[:, None]
+    iq[:, -37:] = (5 * rng.standard_normal((F, 37))).astype(np.complex64)
+    iq = iq.astype(np.complex64)
+    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=False)
+    res = plan.run(torch.from_numpy(iq).cuda())
+    torch.cuda.synchronize()
+    assert plan.last_kernels() == SPEC
+    syms = res.symbols.cpu().numpy()
+    cfo = res.cfo.cpu().numpy()
+    for f in range(0, F, 7):
+        osym, osync, ocfo, otoff = O.lora_demodulate(iq[f], sf, 1, False)
+        np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
+        assert bits(cfo[f]) == bits(ocfo)
+        assert int(res.sync[f]) == osync
+        assert bits(res.time_offset[f].item()) == bits(otoff)
