@@ -1111,9 +1111,12 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     //      word, and each speculative symbol either certified (its margin exceeds the
     //      rounding bound, so the reference's argmax is the same bin) or recomputed exactly.
     // A frame that needs no rescaling (max <= 1) is exact as computed.  The IQ is read once
-    // plus symbols 0/1 twice; lora_demod_spec_recomputed() counts recomputations.
+    // plus symbols 0/1 twice; lora_demod_spec_recomputed() counts recomputations.  Under
+    // LORA_PRECISION_FAST step 2 rotates with the hardware sine/cosine and step 3 certifies
+    // those symbols against the EXACT reference (a wider bound), so rescaled frames come
+    // out exact; unscaled frames keep the FAST symbols, as the three-launch path has them.
     const bool spec_ok = !fused && plan->use_fast && plan->spec && p.mode == LORA_MODE_LEGACY && p.osr == 1 &&
-                         !a.hann && !a.fast_rot && !a.ablate && p.sf >= 6 && total >= 3 &&
+                         !a.hann && !a.ablate && p.sf >= 6 && total >= 3 &&
                          total - 2 + 1 <= lora::kMaxBpf;
     bool spec_done = false;
     if (spec_ok) {

@@ -961,7 +961,11 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         // sum_i |y_i| <= sum_i (|re_i| + |im_i|) <= 2 N max(|re|, |im|) over the window
         const double n1 = 2.0 * N * (double)__uint_as_float(a.spec_max[f * a.mx_bpf + j]);
         const double L = (double)(2 + j) * N + tabs + N;  // |phase argument| scale of symbol 2+j
-        const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E);
+        // LORA_PRECISION_FAST: the speculative rotation used the hardware sine/cosine on
+        // the phase in revolutions (fp32 product with 1/2pi: 2 eps |ph| rad, the unit's own
+        // error well under 1e-4 rad), certified against the exact reference
+        const double fastd = a.fast_rot ? 4.0 * eps * rmax * L + 1e-4 : 0.0;
+        const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E + fastd);
         const bool ok = same_t && (double)d > 4.0 * B;
         if (!ok) atomicOr(&fmask[g][j >> 6], 1ull << (j & 63));
       }
@@ -1404,9 +1408,13 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   } else {
     const int64_t work = frames * (int64_t)(a.total - 2);
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
-    if (stage == 1)
+    if (stage == 1) {
+      if (a.fast_rot)
+        return a.dechirp ? launch_mode<SF, 0, 0, true, true>(a, 2, work, st)
+                         : launch_mode<SF, 1, 0, true, true>(a, 2, work, st);
       return a.dechirp ? launch_mode<SF, 0, 0, false, true>(a, 2, work, st)
                        : launch_mode<SF, 1, 0, false, true>(a, 2, work, st);
+    }
     return a.dechirp ? launch_est_mode<SF, 0, 2>(a, frames, st) : launch_est_mode<SF, 1, 2>(a, frames, st);
   }
 }

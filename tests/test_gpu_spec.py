@@ -224,3 +224,25 @@ def test_ragged_tail_and_many_frames(O, amd):
         assert bits(cfo[f]) == bits(ocfo)
         assert int(res.sync[f]) == osync
         assert bits(res.time_offset[f].item()) == bits(otoff)
+
+
+@pytest.mark.parametrize("sf,snr_db", [(7, 20), (7, -10), (9, 0), (12, 10)])
+def test_fast_precision_rescaled_frames_are_exact(O, amd, sf, snr_db):
+    """LORA_PRECISION_FAST in the pipeline: the hardware-sin/cos symbols of rescaled frames
+    are certified against the EXACT reference (bound widened by the rotation's phase
+    error) or recomputed exactly, so every output equals the oracle's."""
+    rng = np.random.default_rng(700 + sf + snr_db)
+    amp = 2.0
+    noise = amp * 10 ** (-snr_db / 20) / np.sqrt(2)
+    iq = modulated(O, rng, sf, 10 if sf < 12 else 5, 8 if sf < 12 else 3, amp=amp, noise=noise)
+    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=False, precision="fast")
+    res = plan.run(torch.from_numpy(iq).cuda())
+    torch.cuda.synchronize()
+    assert plan.last_kernels() == SPEC
+    syms = res.symbols.cpu().numpy()
+    for f in range(iq.shape[0]):
+        osym, osync, ocfo, otoff = O.lora_demodulate(iq[f], sf, 1, False)
+        np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
+        assert int(res.sync[f]) == osync
+        assert bits(res.cfo[f].item()) == bits(ocfo)
+        assert bits(res.time_offset[f].item()) == bits(otoff)

@@ -71,7 +71,8 @@ def main():
         runs = [json.loads(l) for l in open(os.path.join(src, "kt.log")) if l.startswith("{")]
         for r in runs:
             st = r["config"]["stage_ms"]
-            lines += ["", "bench.py HIP-event averages in the same profiled run (ms): SF7 frame max "
+            lines += ["", "bench.py HIP-event averages in the same profiled run (ms; with the speculative "
+                      "pipeline `estimate` = pre-pass + certification kernels, no frame-max pass): SF7 frame max "
                       f"{st[0]:.4f}, estimate {st[1]:.4f}, demod {st[2]:.4f}"]
             if "sf12" in r.get("extra", {}):
                 s12 = r["extra"]["sf12"]["stage_ms"]
@@ -88,15 +89,21 @@ def main():
         nfirst = 2 + 10 + 10  # warmup + steps + bench.py's profiled pass (kernel-trace command)
         lines += ["", f"Headline SF7 run only (first {nfirst} launches of each kernel, in trace order):", ""]
         fm_starts = []
-        for kn in ("k_frame_max", "k_est_fast<7, 0>", "k_demod_fast<7, 0, 0, false>"):
+        names = {short(n) for n, _, _ in rows}
+        # the default speculative pipeline (est pre-pass, demod, est/certify) or the
+        # three-launch path (frame max, estimate, demod); the first kernel opens each step
+        step_kernels = (("k_est_fast<7, 0, 1>", "k_demod_fast<7, 0, 0, false, true>", "k_est_fast<7, 0, 2>")
+                        if "k_est_fast<7, 0, 1>" in names else
+                        ("k_frame_max", "k_est_fast<7, 0, 0>", "k_demod_fast<7, 0, 0, false, false>"))
+        for kn in step_kernels:
             d = [(b, e) for n, b, e in rows if short(n) == kn][:nfirst]
-            if kn == "k_frame_max":
+            if kn == step_kernels[0]:
                 fm_starts = [b for b, _ in d]
             avg = sum(e - b for b, e in d) / max(len(d), 1) / 1e3
             lines.append(f"- `{kn}`: {len(d)} launches, average {avg:.2f} us")
         if len(fm_starts) >= 12:
             steps = [(fm_starts[i + 1] - fm_starts[i]) / 1e6 for i in range(2, 11)]
-            lines.append(f"- step period from the trace (frame-max start to start, timed steps): "
+            lines.append(f"- step period from the trace (`{step_kernels[0]}` start to start, timed steps): "
                          f"{sum(steps) / len(steps):.4f} ms")
     except (sqlite3.Error, OSError):
         pass
