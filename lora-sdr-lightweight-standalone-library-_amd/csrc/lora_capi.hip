@@ -130,9 +130,10 @@ size_t ws_counter_bytes(int64_t frames) {  // partial maxima, kMaxBpf per frame
 size_t ws_params_bytes(int64_t frames) {  // FrameParams per frame
   return ((size_t)frames * sizeof(lora::FrameParams) + 255) & ~size_t(255);
 }
-// speculative pipeline: pre-pass FrameParams + one margin per data symbol (<= kMaxBpf - 1)
+// speculative pipeline: pre-pass FrameParams + (margin, window max) per data symbol
+// (<= kMaxBpf - 1 of them)
 size_t ws_spec_bytes(int64_t frames) {
-  return ws_params_bytes(frames) + (((size_t)frames * (lora::kMaxBpf - 1) * sizeof(float) + 255) & ~size_t(255));
+  return ws_params_bytes(frames) + (((size_t)frames * (lora::kMaxBpf - 1) * 2 * sizeof(float) + 255) & ~size_t(255));
 }
 
 // ---------------------------------------------------------------------------------
@@ -1121,7 +1122,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     bool spec_done = false;
     if (spec_ok) {
       KArgs as = a;
-      as.mx_bpf = (int)(total - 2) + 1;
+      as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows
       as.maxbits = maxbits;
       bool ok;
       {

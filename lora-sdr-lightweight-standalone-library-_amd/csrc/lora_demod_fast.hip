@@ -518,6 +518,15 @@ __device__ __forceinline__ uint64_t symbol_key(uint64_t key, int tid, uint64_t* 
   }
 }
 
+// max(m, |v.re|, |v.im|) in one instruction (fmaxf would canonicalize each operand).
+// Callers pin the running maximum with an empty volatile asm next to the loads it
+// consumes: left to itself the compiler sinks the chain to the maximum's use after the
+// FFT and keeps every input live until then.
+__device__ __forceinline__ float amax3(float m, cf v) {
+  asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(m) : "v"(v.re), "v"(v.im));
+  return m;
+}
+
 // Speculative demod (SPEC): the maxima of `a` and `b` over the symbol's T lanes (every
 // lane gets them).  Wave-local groups use shuffles; T > 64 adds one LDS round through
 // `rf` (2 floats per wave), which must not alias live data.
@@ -567,10 +576,9 @@ constexpr int demod_waves_per_eu() {
 }
 
 // SPEC: the speculative single-read pipeline's symbol pass (lora_capi.hip): the pre-pass
-// offsets (fp_spec) on unscaled samples, and per data symbol its window's partial
-// max(|I|,|Q|) (spec_max, slot s - s0 of the frame) and the margin |X1| - |X2| between
-// the top bin and the runner-up (spec_marg), which k_est_fast<SPEC = 2> uses to certify
-// or recompute the symbol.
+// offsets (fp_spec) on unscaled samples, and per data symbol (spec_marg, one 8-byte
+// store) the margin |X1| - |X2| between the top bin and the runner-up and the window's
+// max(|I|,|Q|), which k_est_fast<SPEC = 2> uses to normalise, certify or recompute.
 template <int SF, int MODE, int ABL = 0, bool FAST = false, bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
@@ -609,11 +617,8 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   gather_points<SF, ABL>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, scale, in);
   float pm = 0.0f;
   if constexpr (SPEC && !LORA_SPEC_ABL) {  // the window's dechirped, unscaled samples (scale is 1 here)
-    // max(pm, |re|, |im|) in one instruction per point (fmaxf would canonicalize each
-    // operand first); pinned here, as the samples arrive: left to itself the compiler
-    // sinks it to its only use after the FFT and keeps all 2P inputs live (spills).
 #pragma unroll
-    for (int q = 0; q < P; ++q) asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(pm) : "v"(in[q].re), "v"(in[q].im));
+    for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
   }
   rotate_place<SF, !RAW, ABL, FAST>(in, z, start, p.rate, hann, a.win, l);
   if constexpr (SPEC && !LORA_SPEC_ABL) asm volatile("" : "+v"(pm));
@@ -628,8 +633,7 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
     group_reduce2<SF>(r2, pm, tid, reinterpret_cast<float*>(smem + 64));
     if (l == 0 && valid) {
       const int64_t per = a.total - s0;
-      a.spec_marg[f * per + (s - s0)] = sqrtf(key_value(key)) - sqrtf(r2);
-      a.spec_max[f * a.mx_bpf + (s - s0)] = __float_as_uint(pm);
+      reinterpret_cast<float2*>(a.spec_marg)[f * per + (s - s0)] = make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm);
     }
   }
 }
@@ -693,8 +697,21 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   // LoRaDemod.cpp:59-67 max_amp from the frame's partials: the group's lanes load them
   // in parallel (up to kMaxBpf, one dependent load chain per lane is latency-bound)
   float maxv = 0.0f;
+  constexpr int NPL = (kMaxBpf + T - 1) / T;  // SPEC == 2: data symbols per lane, at most
   if (legacy && SPEC != 1) {
-    for (int c = l; c < a.mx_bpf; c += T) maxv = fmaxf(maxv, __uint_as_float(a.maxbits[f * a.mx_bpf + c]));
+    if constexpr (SPEC == 2) {
+      // the pre-pass's slot (samples outside the data windows) and every data window's
+      // maximum from the demod's (margin, max) pairs; all loads issued together
+      maxv = __uint_as_float(a.maxbits[f]);
+      const int per = a.total - 2;
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) {
+        const int j = l + i * T;
+        if (j < per) maxv = fmaxf(maxv, a.spec_marg[2 * (f * per + j) + 1]);
+      }
+    } else {
+      for (int c = l; c < a.mx_bpf; c += T) maxv = fmaxf(maxv, __uint_as_float(a.maxbits[f * a.mx_bpf + c]));
+    }
     maxv = __uint_as_float((uint32_t)(symbol_key<SF>((uint64_t)__float_as_uint(maxv) << 32, tid, red) >> 32));
   }
   const int scaled = maxv > 1.0f;
@@ -721,6 +738,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   bool have_prev = false;
   unsigned sum_t = 0;
   cf in[P], z[P];
+  float mo = 0.0f;  // SPEC == 1: max(|I|,|Q|) over symbols 0/1 (the estimate's gathers)
   constexpr bool PAIR = EstGeo<SF>::PAIR && MODE <= 1;  // MODE 2 (osr / window) would spill
   if constexpr (PAIR) {
     // symbols 0 and 1 in lockstep (fft_key2); the per-symbol bookkeeping below is the
@@ -734,6 +752,11 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     for (int t = 0; t < osr; ++t) {
       gather_points<SF, 0>(a, x + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in);
       gather_points<SF, 0>(a, x + (int64_t)step + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in1);
+      if constexpr (SPEC == 1) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) mo = amax3(amax3(mo, in[q]), in1[q]);
+        asm volatile("" : "+v"(mo));
+      }
       rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
       rotate_place<SF, false, 0>(in1, z1, 0.0f, 0.0f, hann, a.win, l);
       uint64_t key[2];
@@ -786,6 +809,11 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     for (int t = 0; t < osr; ++t) {
       gather_points<SF, 0>(a, x + (int64_t)s * step + t, l, osr, step, t, legacy ? 1 : 0, dech,
                            scale, in);
+      if constexpr (SPEC == 1) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) mo = amax3(mo, in[q]);
+        asm volatile("" : "+v"(mo));
+      }
       rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
       uint64_t key = fft_key<SF, true, 0>(z, row, l, a);
       key = symbol_key<SF>(key, tid, red);
@@ -865,15 +893,17 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   if constexpr (SPEC == 1) {
     // The samples outside every data-symbol window of the pre-pass offsets: [0, start of
     // symbol 2's window) and [end of the last window, frame_len).  With the windows'
-    // partial maxima (k_demod_fast<SPEC>) they make up the whole frame's maximum.
+    // maxima (k_demod_fast<SPEC>) they make up the whole frame's maximum; a sample counted
+    // twice changes nothing, so [0, 2N) comes from the estimate's own gathers (osr 1) and
+    // only a positive t_off's [2N, 2N + t_off) and a tail are read here.
     const int per = a.total - 2;
     int64_t b2, bl;
     int cg;
     sym_base(2, step, a.frame_len, q.t_off, b2, cg);
     sym_base(a.total - 1, step, a.frame_len, q.t_off, bl, cg);
     const int64_t xend = bl + step;
-    float m = 0.0f;
-    for (int64_t j = l; j < b2; j += T) {
+    float m = mo;
+    for (int64_t j = 2 * (int64_t)step + l; j < b2; j += T) {
       cf v = x[j];
       if (dech) v = cmul(v, a.down[j % step]);
       m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
@@ -884,7 +914,8 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
     }
     const uint64_t mk = symbol_key<SF>((uint64_t)__float_as_uint(m) << 32, tid, red);
-    if (l == 0 && valid) a.spec_max[f * a.mx_bpf + per] = (uint32_t)(mk >> 32);
+    (void)per;
+    if (l == 0 && valid) a.spec_max[f] = (uint32_t)(mk >> 32);
     // Already above 1: the frame is rescaled, so k_est_fast<SPEC = 2> recomputes the
     // estimate and the sync word; skip them here (frame-uniform exit).
     if (__uint_as_float((uint32_t)(mk >> 32)) > 1.0f) return;
@@ -956,19 +987,29 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       const double drate = fabs((double)q.rate - (double)qs.rate);
       const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
       const double tabs = (double)abs(q.t_off);
-      for (int j = l; j < per; j += T) {
-        const float d = a.spec_marg[f * per + j];
-        // sum_i |y_i| <= sum_i (|re_i| + |im_i|) <= 2 N max(|re|, |im|) over the window
-        const double n1 = 2.0 * N * (double)__uint_as_float(a.spec_max[f * a.mx_bpf + j]);
-        const double L = (double)(2 + j) * N + tabs + N;  // |phase argument| scale of symbol 2+j
-        // LORA_PRECISION_FAST: the speculative rotation used the hardware sine/cosine on
-        // the phase in revolutions (fp32 product with 1/2pi: 2 eps |ph| rad, the unit's own
-        // error well under 1e-4 rad), certified against the exact reference
-        const double fastd = a.fast_rot ? 4.0 * eps * rmax * L + 1e-4 : 0.0;
-        const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E + fastd);
-        const bool ok = same_t && (double)d > 4.0 * B;
-        if (!ok) atomicOr(&fmask[g][j >> 6], 1ull << (j & 63));
+      uint32_t bad = 0;  // bit i: symbol l + i*T failed (all loads issued before any test)
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) {
+        const int j = l + i * T;
+        if (j < per) {
+          const float2 v = reinterpret_cast<const float2*>(a.spec_marg)[f * per + j];
+          const float d = v.x;
+          // sum_i |y_i| <= sum_i (|re_i| + |im_i|) <= 2 N max(|re|, |im|) over the window
+          const double n1 = 2.0 * N * (double)v.y;
+          const double L = (double)(2 + j) * N + tabs + N;  // |phase argument| scale of symbol 2+j
+          // LORA_PRECISION_FAST: the speculative rotation used the hardware sine/cosine on
+          // the phase in revolutions (fp32 product with 1/2pi: 2 eps |ph| rad, the unit's own
+          // error well under 1e-4 rad), certified against the exact reference
+          const double fastd = a.fast_rot ? 4.0 * eps * rmax * L + 1e-4 : 0.0;
+          const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E + fastd);
+          if (!(same_t && (double)d > 4.0 * B)) bad |= 1u << i;
+        }
       }
+      for (int i = 0; i < NPL; ++i)
+        if (bad >> i & 1) {
+          const int j = l + i * T;
+          atomicOr(&fmask[g][j >> 6], 1ull << (j & 63));
+        }
     }
     block_sync<G::WAVE_LOCAL>();
     const unsigned long long fm0 = fmask[g][0], fm1 = fmask[g][1];

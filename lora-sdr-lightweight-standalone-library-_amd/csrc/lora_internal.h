@@ -38,8 +38,8 @@ struct KArgs {
   // the estimate on unscaled samples, the data symbols' window maxima and certification
   // margins written by the symbol demod, and a device counter of exact recomputations.
   FrameParams* fp_spec = nullptr;  // [frame] estimate on unscaled samples
-  float* spec_marg = nullptr;      // [frame][data symbol]: |X1| - |X2| of the speculative spectrum
-  uint32_t* spec_max = nullptr;    // writable alias of maxbits
+  float* spec_marg = nullptr;      // [frame][data symbol][2]: |X1| - |X2|, window max(|I|,|Q|)
+  uint32_t* spec_max = nullptr;    // writable alias of maxbits: [frame] max outside the windows
   unsigned int* spec_fix = nullptr;
 };
 
@@ -91,7 +91,7 @@ bool launch_fused(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st
 // symbols (lora_capi.hip): stage 0 = k_est_fast<SPEC=1> (estimate on unscaled samples +
 // the maximum outside the data windows), 1 = k_demod_fast<SPEC> (every data symbol, window
 // maxima and certification margins), 2 = k_est_fast<SPEC=2> (exact estimate, outputs,
-// sync word, certification and exact recomputation).  a.mx_bpf = data symbols + 1.
+// sync word, certification and exact recomputation).  a.mx_bpf = 1.
 bool launch_spec(const KArgs& a, int64_t frames, int stage, hipStream_t st);
 
 // Offset estimate + sync symbols with the same FFT machinery, one lane group per frame
