@@ -674,6 +674,7 @@ struct lora_demod_plan {
   int max_chunks;  // 2-stream pipeline depth (LORA_MI355X_CHUNKS, default 1 = off)
   size_t fused_lds_max;  // frame-resident single-read kernel: LDS image limit (0 = off)
   int spec;              // speculative single-read pipeline enabled (LORA_MI355X_SPEC, default 1)
+  int spec_hw;           // ... with the hardware-sin/cos rotation + certification (LORA_MI355X_SPEC_HW, default 1)
   unsigned int* spec_fix = nullptr;  // device counter of symbols the pipeline recomputed
   int last_kernels = 0;  // LORA_KERNEL_* mask of the last lora_demod_batch call
   // Two-stream pipeline: per-frame prep (max + estimate) of chunk c+1 on `aux`
@@ -834,6 +835,8 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
     // its per-frame estimate chain is serial latency that two frames per CU cannot hide.
     const char* sp = std::getenv("LORA_MI355X_SPEC");
     plan->spec = !(sp && sp[0] == '0');
+    const char* sh = std::getenv("LORA_MI355X_SPEC_HW");
+    plan->spec_hw = !(sh && sh[0] == '0');
     const char* fu = std::getenv("LORA_MI355X_FUSED");
     const int fk = fu ? std::max(0, std::min(160, std::atoi(fu))) : 0;
     plan->fused_lds_max = fk == 0 ? 0 : (size_t)fk * 1024 - (fk <= 80 ? 256 : 128);
@@ -1122,6 +1125,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     bool spec_done = false;
     if (spec_ok) {
       KArgs as = a;
+      as.spec_hw = plan->spec_hw;
       as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows
       as.maxbits = maxbits;
       bool ok;

@@ -718,7 +718,9 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   const float scale = scaled ? 1.0f / maxv : 1.0f;
   if constexpr (SPEC == 2) {
     // max <= 1: no rescaling, so the pre-pass estimate, its sync word and every
-    // speculative symbol are already the reference's (identical inputs and arithmetic).
+    // speculative symbol are already the reference's (identical inputs and arithmetic) -
+    // unless the symbols were rotated with the hardware sine/cosine (spec_hw), in which
+    // case the frame goes through the certification below like a rescaled one.
     // Frame-uniform exit: T-lane groups are whole waves or lie within one, and waves that
     // have ended drop out of the other frames' later s_barriers.
     if (!scaled) {
@@ -730,66 +732,132 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         if (a.max_amp) a.max_amp[f] = maxv;
         if (a.sync) a.sync[f] = (uint8_t)qs.pad0;
       }
-      return;
+      if (!a.spec_hw) return;
     }
   }
+  // The frame's exact offsets: estimated below, or for an unscaled frame of the
+  // speculative pipeline the pre-pass's (identical), whose symbols are then certified.
+  FrameParams q;
+  if (SPEC == 2 && !scaled) {
+    q = a.fp_spec[f];
+  } else {
 
-  float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
-  bool have_prev = false;
-  unsigned sum_t = 0;
-  cf in[P], z[P];
-  float mo = 0.0f;  // SPEC == 1: max(|I|,|Q|) over symbols 0/1 (the estimate's gathers)
-  constexpr bool PAIR = EstGeo<SF>::PAIR && MODE <= 1;  // MODE 2 (osr / window) would spill
-  if constexpr (PAIR) {
-    // symbols 0 and 1 in lockstep (fft_key2); the per-symbol bookkeeping below is the
-    // same, applied in the same order (symbol 0 first)
-    cf* row1 = row + (size_t)EstGeo<SF>::SPB * rowc;
-    cf in1[P], z1[P];
-    float bp[2] = {-1e30f, -1e30f}, bfi[2] = {0.0f, 0.0f};
-    uint32_t bidx[2] = {0, 0};
-    unsigned bt[2] = {0, 0};
-    cf bbin[2] = {cf{0.0f, 0.0f}, cf{0.0f, 0.0f}};
-    for (int t = 0; t < osr; ++t) {
-      gather_points<SF, 0>(a, x + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in);
-      gather_points<SF, 0>(a, x + (int64_t)step + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in1);
-      if constexpr (SPEC == 1) {
+    float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
+    bool have_prev = false;
+    unsigned sum_t = 0;
+    cf in[P], z[P];
+    float mo = 0.0f;  // SPEC == 1: max(|I|,|Q|) over symbols 0/1 (the estimate's gathers)
+    constexpr bool PAIR = EstGeo<SF>::PAIR && MODE <= 1;  // MODE 2 (osr / window) would spill
+    if constexpr (PAIR) {
+      // symbols 0 and 1 in lockstep (fft_key2); the per-symbol bookkeeping below is the
+      // same, applied in the same order (symbol 0 first)
+      cf* row1 = row + (size_t)EstGeo<SF>::SPB * rowc;
+      cf in1[P], z1[P];
+      float bp[2] = {-1e30f, -1e30f}, bfi[2] = {0.0f, 0.0f};
+      uint32_t bidx[2] = {0, 0};
+      unsigned bt[2] = {0, 0};
+      cf bbin[2] = {cf{0.0f, 0.0f}, cf{0.0f, 0.0f}};
+      for (int t = 0; t < osr; ++t) {
+        gather_points<SF, 0>(a, x + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in);
+        gather_points<SF, 0>(a, x + (int64_t)step + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in1);
+        if constexpr (SPEC == 1) {
 #pragma unroll
-        for (int q = 0; q < P; ++q) mo = amax3(amax3(mo, in[q]), in1[q]);
-        asm volatile("" : "+v"(mo));
+          for (int q = 0; q < P; ++q) mo = amax3(amax3(mo, in[q]), in1[q]);
+          asm volatile("" : "+v"(mo));
+        }
+        rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
+        rotate_place<SF, false, 0>(in1, z1, 0.0f, 0.0f, hann, a.win, l);
+        uint64_t key[2];
+        fft_key2<SF, true>(z, z1, row, row1, l, a, key[0], key[1]);
+        key[0] = group_max(key[0], T);
+        key[1] = group_max(key[1], T);
+        if (l == 0) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const cf* rw = s ? row1 : row;
+            const uint32_t idx = key_index(key[s]);
+            const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
+            const cf L = rw[lds_slot<SF>((int)im1)], R = rw[lds_slot<SF>((int)ip1)],
+                     B = rw[lds_slot<SF>((int)idx)];
+            float pw, fi;
+            detect_tail(key_value(key[s]), L, R, a.power_scale, &pw, &fi);
+            if (pw > bp[s] || (legacy && pw == bp[s] && idx < bidx[s])) {
+              bp[s] = pw;
+              bidx[s] = idx;
+              bfi[s] = fi;
+              bt[s] = (unsigned)t;
+              bbin[s] = B;
+            }
+          }
+        }
+        wave_sync();  // the rows are rewritten by the next phase
       }
-      rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
-      rotate_place<SF, false, 0>(in1, z1, 0.0f, 0.0f, hann, a.win, l);
-      uint64_t key[2];
-      fft_key2<SF, true>(z, z1, row, row1, l, a, key[0], key[1]);
-      key[0] = group_max(key[0], T);
-      key[1] = group_max(key[1], T);
       if (l == 0) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const cf* rw = s ? row1 : row;
-          const uint32_t idx = key_index(key[s]);
-          const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
-          const cf L = rw[lds_slot<SF>((int)im1)], R = rw[lds_slot<SF>((int)ip1)],
-                   B = rw[lds_slot<SF>((int)idx)];
-          float pw, fi;
-          detect_tail(key_value(key[s]), L, R, a.power_scale, &pw, &fi);
-          if (pw > bp[s] || (legacy && pw == bp[s] && idx < bidx[s])) {
-            bp[s] = pw;
-            bidx[s] = idx;
-            bfi[s] = fi;
-            bt[s] = (unsigned)t;
-            bbin[s] = B;
+          sum_t += bt[s];
+          sum_index += (float)bidx[s] + bfi[s];
+          const float phase = lm_atan2f(bbin[s].im, bbin[s].re);
+          if (have_prev) {
+            float d = phase - prev_phase;
+            while (d > PI_F) d -= 2.0f * PI_F;
+            while (d < -PI_F) d += 2.0f * PI_F;
+            phase_diff += d;
           }
+          prev_phase = phase;
+          have_prev = true;
         }
       }
-      wave_sync();  // the rows are rewritten by the next phase
     }
-    if (l == 0) {
+    for (int s = 0; s < (PAIR ? 0 : 2); ++s) {
+      float best_p = -1e30f, best_fi = 0.0f;
+      uint32_t best_idx = 0;
+      unsigned best_t = 0;
+      cf best_bin = {0.0f, 0.0f};
+      for (int t = 0; t < osr; ++t) {
+        gather_points<SF, 0>(a, x + (int64_t)s * step + t, l, osr, step, t, legacy ? 1 : 0, dech,
+                             scale, in);
+        if constexpr (SPEC == 1) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        sum_t += bt[s];
-        sum_index += (float)bidx[s] + bfi[s];
-        const float phase = lm_atan2f(bbin[s].im, bbin[s].re);
+          for (int q = 0; q < P; ++q) mo = amax3(mo, in[q]);
+          asm volatile("" : "+v"(mo));
+        }
+        rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
+        uint64_t key = fft_key<SF, true, 0>(z, row, l, a);
+        key = symbol_key<SF>(key, tid, red);
+        if (l == 0) {
+          const uint32_t idx = key_index(key);
+          const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
+          cf L, R, B;
+          if constexpr (G::NPASS == 1) {
+            L = R = B = cf{0.0f, 0.0f};
+#pragma unroll
+            for (int u = 0; u < N; ++u) {
+              if ((uint32_t)u == im1) L = z[u];
+              if ((uint32_t)u == ip1) R = z[u];
+              if ((uint32_t)u == idx) B = z[u];
+            }
+          } else {
+            L = row[lds_slot<SF>((int)im1)];
+            R = row[lds_slot<SF>((int)ip1)];
+            B = row[lds_slot<SF>((int)idx)];
+          }
+          float pw, fi;
+          detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
+          if (pw > best_p || (legacy && pw == best_p && idx < best_idx)) {
+            best_p = pw;
+            best_idx = idx;
+            best_fi = fi;
+            best_t = (unsigned)t;
+            best_bin = B;
+          }
+        }
+        block_sync<G::WAVE_LOCAL>();  // row is rewritten by the next transform
+      }
+      if (l == 0) {
+        sum_t += best_t;
+        sum_index += (float)best_idx + best_fi;
+        const float phase = lm_atan2f(best_bin.im, best_bin.re);
         if (have_prev) {
           float d = phase - prev_phase;
           while (d > PI_F) d -= 2.0f * PI_F;
@@ -800,170 +868,111 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         have_prev = true;
       }
     }
-  }
-  for (int s = 0; s < (PAIR ? 0 : 2); ++s) {
-    float best_p = -1e30f, best_fi = 0.0f;
-    uint32_t best_idx = 0;
-    unsigned best_t = 0;
-    cf best_bin = {0.0f, 0.0f};
-    for (int t = 0; t < osr; ++t) {
-      gather_points<SF, 0>(a, x + (int64_t)s * step + t, l, osr, step, t, legacy ? 1 : 0, dech,
-                           scale, in);
-      if constexpr (SPEC == 1) {
-#pragma unroll
-        for (int q = 0; q < P; ++q) mo = amax3(mo, in[q]);
-        asm volatile("" : "+v"(mo));
-      }
-      rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
-      uint64_t key = fft_key<SF, true, 0>(z, row, l, a);
-      key = symbol_key<SF>(key, tid, red);
-      if (l == 0) {
-        const uint32_t idx = key_index(key);
-        const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
-        cf L, R, B;
-        if constexpr (G::NPASS == 1) {
-          L = R = B = cf{0.0f, 0.0f};
-#pragma unroll
-          for (int u = 0; u < N; ++u) {
-            if ((uint32_t)u == im1) L = z[u];
-            if ((uint32_t)u == ip1) R = z[u];
-            if ((uint32_t)u == idx) B = z[u];
-          }
-        } else {
-          L = row[lds_slot<SF>((int)im1)];
-          R = row[lds_slot<SF>((int)ip1)];
-          B = row[lds_slot<SF>((int)idx)];
-        }
-        float pw, fi;
-        detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
-        if (pw > best_p || (legacy && pw == best_p && idx < best_idx)) {
-          best_p = pw;
-          best_idx = idx;
-          best_fi = fi;
-          best_t = (unsigned)t;
-          best_bin = B;
-        }
-      }
-      block_sync<G::WAVE_LOCAL>();  // row is rewritten by the next transform
-    }
     if (l == 0) {
-      sum_t += best_t;
-      sum_index += (float)best_idx + best_fi;
-      const float phase = lm_atan2f(best_bin.im, best_bin.re);
-      if (have_prev) {
-        float d = phase - prev_phase;
-        while (d > PI_F) d -= 2.0f * PI_F;
-        while (d < -PI_F) d += 2.0f * PI_F;
-        phase_diff += d;
-      }
-      prev_phase = phase;
-      have_prev = true;
-    }
-  }
-  if (l == 0) {
-    const float avg_index = sum_index / 2.0f;
-    const float cfo_coarse = avg_index / (float)N;
-    const float cfo_fine = (phase_diff / 1.0f) / (2.0f * PI_F * (float)N);
-    const float cfo = cfo_coarse + cfo_fine;
-    const float frac = avg_index - floorf(avg_index + 0.5f);
-    const float avg_t = (float)sum_t / 2.0f;
-    const float toff = avg_t - frac * (float)N * (float)osr;
-    FrameParams q;
-    q.cfo = cfo;
-    q.toff = toff;
-    q.t_off = (int)roundf(toff);
-    q.rate = -2.0f * PI_F * cfo / (float)N;
-    q.scale = scale;
-    q.scaled = scaled;
-    q.pad0 = q.pad1 = 0;
-    sp[g] = q;
-    if (valid) {
-      if constexpr (SPEC == 1) {
-        a.fp_spec[f] = q;
-      } else {
-        a.fp[f] = q;
-        if (a.cfo) a.cfo[f] = cfo;
-        if (a.toff) a.toff[f] = toff;
-        if (a.max_amp) a.max_amp[f] = maxv;
+      const float avg_index = sum_index / 2.0f;
+      const float cfo_coarse = avg_index / (float)N;
+      const float cfo_fine = (phase_diff / 1.0f) / (2.0f * PI_F * (float)N);
+      const float cfo = cfo_coarse + cfo_fine;
+      const float frac = avg_index - floorf(avg_index + 0.5f);
+      const float avg_t = (float)sum_t / 2.0f;
+      const float toff = avg_t - frac * (float)N * (float)osr;
+      FrameParams qe;
+      qe.cfo = cfo;
+      qe.toff = toff;
+      qe.t_off = (int)roundf(toff);
+      qe.rate = -2.0f * PI_F * cfo / (float)N;
+      qe.scale = scale;
+      qe.scaled = scaled;
+      qe.pad0 = qe.pad1 = 0;
+      sp[g] = qe;
+      if (valid) {
+        if constexpr (SPEC == 1) {
+          a.fp_spec[f] = qe;
+        } else {
+          a.fp[f] = qe;
+          if (a.cfo) a.cfo[f] = cfo;
+          if (a.toff) a.toff[f] = toff;
+          if (a.max_amp) a.max_amp[f] = maxv;
+        }
       }
     }
-  }
-  block_sync<G::WAVE_LOCAL>();
-  const FrameParams q = sp[g];
-  if constexpr (SPEC == 1) {
-    // The samples outside every data-symbol window of the pre-pass offsets: [0, start of
-    // symbol 2's window) and [end of the last window, frame_len).  With the windows'
-    // maxima (k_demod_fast<SPEC>) they make up the whole frame's maximum; a sample counted
-    // twice changes nothing, so [0, 2N) comes from the estimate's own gathers (osr 1) and
-    // only a positive t_off's [2N, 2N + t_off) and a tail are read here.
-    const int per = a.total - 2;
-    int64_t b2, bl;
-    int cg;
-    sym_base(2, step, a.frame_len, q.t_off, b2, cg);
-    sym_base(a.total - 1, step, a.frame_len, q.t_off, bl, cg);
-    const int64_t xend = bl + step;
-    float m = mo;
-    for (int64_t j = 2 * (int64_t)step + l; j < b2; j += T) {
-      cf v = x[j];
-      if (dech) v = cmul(v, a.down[j % step]);
-      m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
-    }
-    for (int64_t j = xend + l; j < a.frame_len; j += T) {
-      cf v = x[j];
-      if (dech) v = cmul(v, a.down[j % step]);
-      m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
-    }
-    const uint64_t mk = symbol_key<SF>((uint64_t)__float_as_uint(m) << 32, tid, red);
-    (void)per;
-    if (l == 0 && valid) a.spec_max[f] = (uint32_t)(mk >> 32);
-    // Already above 1: the frame is rescaled, so k_est_fast<SPEC = 2> recomputes the
-    // estimate and the sync word; skip them here (frame-uniform exit).
-    if (__uint_as_float((uint32_t)(mk >> 32)) > 1.0f) return;
-    block_sync<G::WAVE_LOCAL>();  // red is reused by the sync symbols
-  }
-  uint32_t sw[2];
-  if constexpr (PAIR) {
-    cf* row1 = row + (size_t)EstGeo<SF>::SPB * rowc;
-    cf in1[P], z1[P];
-    int64_t base0, base1;
-    int cg0, cg1;
-    sym_base(0, step, a.frame_len, q.t_off, base0, cg0);
-    sym_base(1, step, a.frame_len, q.t_off, base1, cg1);
-    const float st0 = q.rate * ((float)((uint32_t)0 * (uint32_t)N) + (float)q.t_off / (float)osr);
-    const float st1 = q.rate * ((float)((uint32_t)1 * (uint32_t)N) + (float)q.t_off / (float)osr);
-    const float sc = (legacy && q.scaled) ? q.scale : 1.0f;
-    gather_points<SF, 0>(a, x + base0, l, osr, step, cg0, legacy ? 1 : 2, dech, sc, in);
-    gather_points<SF, 0>(a, x + base1, l, osr, step, cg1, legacy ? 1 : 2, dech, sc, in1);
-    rotate_place<SF, true, 0>(in, z, st0, q.rate, hann, a.win, l);
-    rotate_place<SF, true, 0>(in1, z1, st1, q.rate, hann, a.win, l);
-    uint64_t k0, k1;
-    fft_key2<SF, false>(z, z1, row, row1, l, a, k0, k1);
-    sw[0] = key_index(group_max(k0, T));
-    sw[1] = key_index(group_max(k1, T));
-  }
-  for (int s = 0; s < (PAIR ? 0 : 2); ++s) {
-    int64_t base;
-    int cg;
-    sym_base(s, step, a.frame_len, q.t_off, base, cg);
-    const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
-    gather_points<SF, 0>(a, x + base, l, osr, step, cg, legacy ? 1 : 2, dech,
-                         (legacy && q.scaled) ? q.scale : 1.0f, in);
-    rotate_place<SF, true, 0>(in, z, start, q.rate, hann, a.win, l);
-    uint64_t key = fft_key<SF, false, 0>(z, row, l, a);
-    key = symbol_key<SF>(key, tid, red);
-    sw[s] = key_index(key);
     block_sync<G::WAVE_LOCAL>();
-  }
-  if (l == 0 && valid) {
-    const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
-    const uint8_t word = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
+    q = sp[g];
     if constexpr (SPEC == 1) {
-      a.fp_spec[f].pad0 = word;  // the pre-pass sync word, final when the frame is not rescaled
-    } else if (a.sync) {
-      a.sync[f] = word;
+      // The samples outside every data-symbol window of the pre-pass offsets: [0, start of
+      // symbol 2's window) and [end of the last window, frame_len).  With the windows'
+      // maxima (k_demod_fast<SPEC>) they make up the whole frame's maximum; a sample counted
+      // twice changes nothing, so [0, 2N) comes from the estimate's own gathers (osr 1) and
+      // only a positive t_off's [2N, 2N + t_off) and a tail are read here.
+      const int per = a.total - 2;
+      int64_t b2, bl;
+      int cg;
+      sym_base(2, step, a.frame_len, q.t_off, b2, cg);
+      sym_base(a.total - 1, step, a.frame_len, q.t_off, bl, cg);
+      const int64_t xend = bl + step;
+      float m = mo;
+      for (int64_t j = 2 * (int64_t)step + l; j < b2; j += T) {
+        cf v = x[j];
+        if (dech) v = cmul(v, a.down[j % step]);
+        m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+      }
+      for (int64_t j = xend + l; j < a.frame_len; j += T) {
+        cf v = x[j];
+        if (dech) v = cmul(v, a.down[j % step]);
+        m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+      }
+      const uint64_t mk = symbol_key<SF>((uint64_t)__float_as_uint(m) << 32, tid, red);
+      (void)per;
+      if (l == 0 && valid) a.spec_max[f] = (uint32_t)(mk >> 32);
+      // Already above 1: the frame is rescaled, so k_est_fast<SPEC = 2> recomputes the
+      // estimate and the sync word; skip them here (frame-uniform exit).
+      if (__uint_as_float((uint32_t)(mk >> 32)) > 1.0f) return;
+      block_sync<G::WAVE_LOCAL>();  // red is reused by the sync symbols
     }
-  }
-  if constexpr (SPEC == 1) return;
+    uint32_t sw[2];
+    if constexpr (PAIR) {
+      cf* row1 = row + (size_t)EstGeo<SF>::SPB * rowc;
+      cf in1[P], z1[P];
+      int64_t base0, base1;
+      int cg0, cg1;
+      sym_base(0, step, a.frame_len, q.t_off, base0, cg0);
+      sym_base(1, step, a.frame_len, q.t_off, base1, cg1);
+      const float st0 = q.rate * ((float)((uint32_t)0 * (uint32_t)N) + (float)q.t_off / (float)osr);
+      const float st1 = q.rate * ((float)((uint32_t)1 * (uint32_t)N) + (float)q.t_off / (float)osr);
+      const float sc = (legacy && q.scaled) ? q.scale : 1.0f;
+      gather_points<SF, 0>(a, x + base0, l, osr, step, cg0, legacy ? 1 : 2, dech, sc, in);
+      gather_points<SF, 0>(a, x + base1, l, osr, step, cg1, legacy ? 1 : 2, dech, sc, in1);
+      rotate_place<SF, true, 0>(in, z, st0, q.rate, hann, a.win, l);
+      rotate_place<SF, true, 0>(in1, z1, st1, q.rate, hann, a.win, l);
+      uint64_t k0, k1;
+      fft_key2<SF, false>(z, z1, row, row1, l, a, k0, k1);
+      sw[0] = key_index(group_max(k0, T));
+      sw[1] = key_index(group_max(k1, T));
+    }
+    for (int s = 0; s < (PAIR ? 0 : 2); ++s) {
+      int64_t base;
+      int cg;
+      sym_base(s, step, a.frame_len, q.t_off, base, cg);
+      const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
+      gather_points<SF, 0>(a, x + base, l, osr, step, cg, legacy ? 1 : 2, dech,
+                           (legacy && q.scaled) ? q.scale : 1.0f, in);
+      rotate_place<SF, true, 0>(in, z, start, q.rate, hann, a.win, l);
+      uint64_t key = fft_key<SF, false, 0>(z, row, l, a);
+      key = symbol_key<SF>(key, tid, red);
+      sw[s] = key_index(key);
+      block_sync<G::WAVE_LOCAL>();
+    }
+    if (l == 0 && valid) {
+      const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
+      const uint8_t word = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
+      if constexpr (SPEC == 1) {
+        a.fp_spec[f].pad0 = word;  // the pre-pass sync word, final when the frame is not rescaled
+      } else if (a.sync) {
+        a.sync[f] = word;
+      }
+    }
+    if constexpr (SPEC == 1) return;
+  }  // exact estimate
   if constexpr (SPEC == 2) {
     // ---- certification of the data symbols the demod computed speculatively ----
     // The demod used the pre-pass offsets qs on unscaled samples y; the reference uses q
@@ -997,10 +1006,14 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
           // sum_i |y_i| <= sum_i (|re_i| + |im_i|) <= 2 N max(|re|, |im|) over the window
           const double n1 = 2.0 * N * (double)v.y;
           const double L = (double)(2 + j) * N + tabs + N;  // |phase argument| scale of symbol 2+j
-          // LORA_PRECISION_FAST: the speculative rotation used the hardware sine/cosine on
-          // the phase in revolutions (fp32 product with 1/2pi: 2 eps |ph| rad, the unit's own
-          // error well under 1e-4 rad), certified against the exact reference
-          const double fastd = a.fast_rot ? 4.0 * eps * rmax * L + 1e-4 : 0.0;
+          // Hardware rotation (spec_hw, LORA_PRECISION_FAST): the demod rotated by
+          // v_sin/v_cos_f32 of fract(fl(ph * fl(1/2pi))) instead of glibc sincosf(ph): the
+          // argument's two roundings move the angle by <= 2 eps |ph| rad, and the unit itself
+          // is within 1.26e-7 of sin/cos(2 pi r) for every fp32 r in [0, 1) (measured
+          // exhaustively, tools/micro/hw_sincos_err.hip), so each rotation factor is off by
+          // < 2 eps |ph| + sqrt(2) * 1.26e-7; doubled here.  Certified against the exact
+          // reference like every other symbol.
+          const double fastd = (a.fast_rot || a.spec_hw) ? 4.0 * eps * rmax * L + 4e-7 : 0.0;
           const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E + fastd);
           if (!(same_t && (double)d > 4.0 * B)) bad |= 1u << i;
         }
@@ -1450,7 +1463,7 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
     const int64_t work = frames * (int64_t)(a.total - 2);
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
     if (stage == 1) {
-      if (a.fast_rot)
+      if (a.fast_rot || a.spec_hw)
         return a.dechirp ? launch_mode<SF, 0, 0, true, true>(a, 2, work, st)
                          : launch_mode<SF, 1, 0, true, true>(a, 2, work, st);
       return a.dechirp ? launch_mode<SF, 0, 0, false, true>(a, 2, work, st)

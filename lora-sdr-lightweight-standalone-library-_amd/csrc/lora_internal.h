@@ -41,6 +41,8 @@ struct KArgs {
   float* spec_marg = nullptr;      // [frame][data symbol][2]: |X1| - |X2|, window max(|I|,|Q|)
   uint32_t* spec_max = nullptr;    // writable alias of maxbits: [frame] max outside the windows
   unsigned int* spec_fix = nullptr;
+  int spec_hw = 0;  // the speculative demod rotates with the hardware sine/cosine; every
+                    // frame's symbols are certified against the exact reference
 };
 
 // Shape of the fast kernels' LDS passes for SF >= 6 (lora_demod_fast.hip Geo<SF>): pass-1

@@ -44,17 +44,22 @@ def bits(x):
     return np.asarray(x, np.float32).view(np.uint32)
 
 
-def check(O, amd, iq, sf, spec=True):
+def check(O, amd, iq, sf, spec=True, hw=True):
     """Run `iq` ([F, L] dechirped frames) through a fresh plan and compare every output
-    with the oracle; returns (plan, recomputed symbols)."""
+    with the oracle; returns (plan, recomputed symbols).  spec=False: three-launch path;
+    hw=False: the speculative demod rotates with glibc sincosf instead of the hardware
+    sine/cosine (LORA_MI355X_SPEC_HW=0)."""
     import os
 
     if not spec:
         os.environ["LORA_MI355X_SPEC"] = "0"
+    if not hw:
+        os.environ["LORA_MI355X_SPEC_HW"] = "0"
     try:
         plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=False)
     finally:
         os.environ.pop("LORA_MI355X_SPEC", None)
+        os.environ.pop("LORA_MI355X_SPEC_HW", None)
     res = plan.run(torch.from_numpy(np.ascontiguousarray(iq)).cuda())
     torch.cuda.synchronize()
     syms = res.symbols.cpu().numpy()
@@ -90,27 +95,36 @@ def modulated(O, rng, sf, S, F, amp=1.0, noise=0.0):
     return out
 
 
+@pytest.mark.parametrize("hw", [True, False])
 @pytest.mark.parametrize("sf", [6, 7, 8, 9, 10, 11, 12])
-def test_verbatim_frames_need_no_recomputation(O, amd, sf):
-    """max(|I|,|Q|) <= 1: the scale is 1, the pre-pass estimate IS the exact one."""
+def test_unscaled_frames(O, amd, sf, hw):
+    """max(|I|,|Q|) <= 1: the scale is 1 and the pre-pass estimate IS the exact one.  With
+    glibc sincosf in the demod (hw=False) every symbol is then exact as computed (nothing
+    to certify, nothing recomputed); with the hardware rotation (default) the symbols are
+    certified, and a frame whose estimated CFO sits near half a bin (two bins of almost
+    equal power in every data symbol, e.g. frame 5 at SF7 here) has a few recomputed."""
     rng = np.random.default_rng(100 + sf)
     iq = modulated(O, rng, sf, 8 if sf < 11 else 5, 6, amp=0.5, noise=0.05)
     assert np.abs(iq.view(np.float32)).max() <= 1.0
-    plan, fixed = check(O, amd, iq, sf)
+    plan, fixed = check(O, amd, iq, sf, hw=hw)
     assert plan.last_kernels() == SPEC
-    assert fixed == 0
+    if hw:
+        assert fixed <= iq.shape[0] * (iq.shape[1] // (1 << sf) - 2) // 4
+    else:
+        assert fixed == 0
 
 
+@pytest.mark.parametrize("hw", [True, False])
 @pytest.mark.parametrize("sf", [6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("snr_db", [20, 0, -10, -15])
-def test_rescaled_frames_match_oracle(O, amd, sf, snr_db):
+def test_rescaled_frames_match_oracle(O, amd, sf, snr_db, hw):
     """max > 1 (rescaled) at high and low SNR: certified or recomputed, always exact."""
     rng = np.random.default_rng(1000 * sf + snr_db + 50)
     amp = 2.5
     noise = amp * 10 ** (-snr_db / 20) / np.sqrt(2)
     iq = modulated(O, rng, sf, 10 if sf < 11 else 5, 8 if sf < 10 else 3, amp=amp, noise=noise)
     assert np.abs(iq.view(np.float32)).max() > 1.0
-    plan, fixed = check(O, amd, iq, sf)
+    plan, fixed = check(O, amd, iq, sf, hw=hw)
     assert plan.last_kernels() == SPEC
     assert fixed >= 0
 
