@@ -158,7 +158,7 @@ __device__ __forceinline__ void block_sync() {
 // for the sign of a zero component, and a zero's sign never reaches a non-zero result
 // or |X|^2, so every bin magnitude - hence the argmax - is bit-identical.  Transforms
 // whose bin values are used (the estimate's phase) keep the multiplies.
-template <int R, bool R2, int N, int MA, bool UNIT = false>
+template <int R, bool R2, int N, int MA, bool UNIT = false, bool FMA = false>
 __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ tw) {
   int S = 1;
   if constexpr (R2) {
@@ -168,7 +168,7 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ t
       if (UNIT)
         bfly2_unit(x[b], x[b + 1]);
       else
-        bfly2(x[b], x[b + 1], tw[k * fs]);
+        bfly2<FMA>(x[b], x[b + 1], tw[k * fs]);
     }
     S = 2;
   }
@@ -183,7 +183,7 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ t
         if (UNIT && uu == 0)
           bfly4_unit(x[blk], x[blk + S], x[blk + 2 * S], x[blk + 3 * S]);
         else
-          bfly4(x[blk + uu], x[blk + uu + S], x[blk + uu + 2 * S], x[blk + uu + 3 * S], tw[kk * fs],
+          bfly4<FMA>(x[blk + uu], x[blk + uu + S], x[blk + uu + 2 * S], x[blk + uu + 3 * S], tw[kk * fs],
                 tw[2 * kk * fs], tw[3 * kk * fs]);
       }
     }
@@ -193,16 +193,16 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, const cf* __restrict__ t
 
 // pass_regs<16, false, N, MA> with the twiddles read from the slot-major copy
 // twT[j*MA + k] (lora::twT_index): the same butterflies, operands and order.
-template <int R, int MA>
+template <int R, int MA, bool FMA = false>
 __device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__ twT) {
   static_assert(R == 4 || R == 16, "radix-4 / radix-16 passes");
 #pragma unroll
   for (int blk = 0; blk < R; blk += 4)
-    bfly4(x[blk], x[blk + 1], x[blk + 2], x[blk + 3], twT[0 * MA + k], twT[1 * MA + k], twT[2 * MA + k]);
+    bfly4<FMA>(x[blk], x[blk + 1], x[blk + 2], x[blk + 3], twT[0 * MA + k], twT[1 * MA + k], twT[2 * MA + k]);
   if constexpr (R == 16) {
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu)
-      bfly4(x[uu], x[uu + 4], x[uu + 8], x[uu + 12], twT[(3 + 3 * uu) * MA + k], twT[(4 + 3 * uu) * MA + k],
+      bfly4<FMA>(x[uu], x[uu + 4], x[uu + 8], x[uu + 12], twT[(3 + 3 * uu) * MA + k], twT[(4 + 3 * uu) * MA + k],
             twT[(5 + 3 * uu) * MA + k]);
   }
 }
@@ -213,7 +213,7 @@ __device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__
 #define LORA_SPEC_ABL 0  // A/B only: 1 = skip the speculative extras (results invalid)
 #endif
 
-template <int R, int N, int MA, int SF, int T, int P, bool LAST>
+template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
                                          uint64_t& key, const cf* __restrict__ twT = nullptr,
                                          float* second = nullptr) {
@@ -228,11 +228,11 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
     if constexpr (R == 4 || R == 16) {
       if (twT) {
-        pass_regs_T<R, MA>(xs, k, twT);
+        pass_regs_T<R, MA, FMA>(xs, k, twT);
         continue;
       }
     }
-    pass_regs<R, false, N, MA>(xs, k, tw);
+    pass_regs<R, false, N, MA, false, FMA>(xs, k, tw);
   }
   if constexpr (LAST) {
     // The last pass covers all N bins with cc == 0: bin = (l + T*gg) + MA*u.  Scanning
@@ -299,7 +299,7 @@ __device__ __forceinline__ void sym_base(int s, int step, int64_t frame_len, int
 // and apply what precedes the rotation: KIND 0 raw (API estimate, phy.cpp:91-99),
 // KIND 1 LEGACY (caller dechirp, e2e_chain_test.cpp:88-93, then normalisation,
 // LoRaDemod.cpp:68-77), KIND 2 API down-chirp (phy.cpp:216-225).
-template <int SF, int ABL>
+template <int SF, int ABL, bool FMA = false>
 __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restrict__ x, int l,
                                               int osr, int step, int cg, int kind, bool dech,
                                               float scale, cf* in) {
@@ -329,7 +329,7 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
         for (int q = 0; q < P; ++q) in[q] = cmul(in[q], d0);
       } else {
 #pragma unroll
-        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[(T * q) * osr]);
+        for (int q = 0; q < P; ++q) in[q] = cmul_t<FMA>(in[q], dl[(T * q) * osr]);
       }
     }
 #pragma unroll
@@ -339,7 +339,7 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 
 // CFO rotation (glibc-faithful sincosf, LoRaDemod.cpp:151-157) when ROT, window
 // (:158-160), and placement in pass-1 leaf order.
-template <int SF, bool ROT, int ABL, bool FAST = false>
+template <int SF, bool ROT, int ABL, bool FAST = false, bool FMA = false>
 __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, float rate,
                                              bool hann, const float* __restrict__ win, int l) {
   using G = Geo<SF>;
@@ -353,7 +353,7 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
     for (int q = 0; q < P; ++q) {
       const float ph = start + rate * (float)(l + T * q);
       const float rev = __builtin_amdgcn_fractf(ph * INV_2PI);
-      cf v = cmul(in[q], cf{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)});
+      cf v = cmul_t<FMA>(in[q], cf{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)});
       if (hann) v = cscale(v, win[l + T * q]);
       z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
     }
@@ -403,14 +403,14 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
 // FFT of the symbol held as pass-1 inputs in z (T lanes x P points) and the lane's
 // argmax key.  KEEP: leave the spectrum in natural order in `row` (padded address
 // paddr(bin)) for the estimate's neighbour bins; NPASS == 1 keeps it in z.
-template <int SF, bool KEEP, int ABL>
+template <int SF, bool KEEP, int ABL, bool FMA = false>
 __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
   constexpr bool WL = G::WAVE_LOCAL;
   if (!(ABL & 2)) {
 #pragma unroll
-    for (int h = 0; h < G::G1; ++h) pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP>(z + h * R1, 0, a.tw);
+    for (int h = 0; h < G::G1; ++h) pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP, FMA>(z + h * R1, 0, a.tw);
   }
   uint64_t key = 0;
   if constexpr (G::NPASS == 1) {
@@ -437,13 +437,13 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
     constexpr int RL = G::NPASS == 2 ? G::RA : G::RB;   // last pass span
     constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, true>(row, z, l, a.tw, key, a.twTA, second);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA>(row, z, l, a.tw, key, a.twTA, second);
     } else {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, false>(row, z, l, a.tw, key, a.twTA);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA>(row, z, l, a.tw, key, a.twTA);
       block_sync<WL>();
       write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
       block_sync<WL>();
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true>(row, z, l, a.tw, key, a.twTB, second);
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA>(row, z, l, a.tw, key, a.twTB, second);
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)
@@ -613,18 +613,21 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   // LoRaDemod.cpp:68-77: scale is 1.0f when the frame is not rescaled (x*1.0f == x).
   const float scale = (legacy && p.scaled) ? p.scale : 1.0f;
 
+  // The speculative demod with the hardware rotation (certified for every frame) also
+  // uses fused multiply-adds for its complex products, and skips the unit scale.
+  constexpr bool FMA = SPEC && FAST;
   cf in[P], z[P];
-  gather_points<SF, ABL>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, scale, in);
+  gather_points<SF, ABL, FMA>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
   float pm = 0.0f;
   if constexpr (SPEC && !LORA_SPEC_ABL) {  // the window's dechirped, unscaled samples (scale is 1 here)
 #pragma unroll
     for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
   }
-  rotate_place<SF, !RAW, ABL, FAST>(in, z, start, p.rate, hann, a.win, l);
+  rotate_place<SF, !RAW, ABL, FAST, FMA>(in, z, start, p.rate, hann, a.win, l);
   if constexpr (SPEC && !LORA_SPEC_ABL) asm volatile("" : "+v"(pm));
   float sec = 0.0f;
   const uint64_t lkey =
-      fft_key<SF, false, ABL>(z, rows + (size_t)g * rowc, l, a, SPEC && !LORA_SPEC_ABL ? &sec : nullptr);
+      fft_key<SF, false, ABL, FMA>(z, rows + (size_t)g * rowc, l, a, SPEC && !LORA_SPEC_ABL ? &sec : nullptr);
   const uint64_t key = symbol_key<SF>(lkey, tid, red);
   if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + (s - s0)] = (uint16_t)key_index(key);
   if constexpr (SPEC && !LORA_SPEC_ABL) {
@@ -1011,7 +1014,9 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
           // argument's two roundings move the angle by <= 2 eps |ph| rad, and the unit itself
           // is within 1.26e-7 of sin/cos(2 pi r) for every fp32 r in [0, 1) (measured
           // exhaustively, tools/micro/hw_sincos_err.hip), so each rotation factor is off by
-          // < 2 eps |ph| + sqrt(2) * 1.26e-7; doubled here.  Certified against the exact
+          // < 2 eps |ph| + sqrt(2) * 1.26e-7; doubled here.  That demod also computes its
+          // complex products with fused multiply-adds: one rounding where the reference has
+          // two, so E bounds its FFT and products as well.  Certified against the exact
           // reference like every other symbol.
           const double fastd = (a.fast_rot || a.spec_hw) ? 4.0 * eps * rmax * L + 4e-7 : 0.0;
           const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E + fastd);

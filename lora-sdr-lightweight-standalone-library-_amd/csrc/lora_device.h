@@ -32,15 +32,26 @@ struct FrameParams {
 __device__ __forceinline__ cf cmul(cf a, cf b) {
   return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
+// FMA = true: the same product with two fused multiply-adds (fewer roundings, not the
+// reference's arithmetic): only for the speculative demod, whose symbols are certified
+// against a rounding bound (lora_demod_fast.hip, k_est_fast<SPEC = 2>).
+template <bool FMA>
+__device__ __forceinline__ cf cmul_t(cf a, cf b) {
+  if constexpr (FMA)
+    return {__builtin_fmaf(a.re, b.re, -(a.im * b.im)), __builtin_fmaf(a.re, b.im, a.im * b.re)};
+  else
+    return cmul(a, b);
+}
 __device__ __forceinline__ cf cadd(cf a, cf b) { return {a.re + b.re, a.im + b.im}; }
 __device__ __forceinline__ cf csub(cf a, cf b) { return {a.re - b.re, a.im - b.im}; }
 __device__ __forceinline__ cf cscale(cf a, float s) { return {a.re * s, a.im * s}; }
 
 // kissfft.hh:164-185 kf_bfly4 (forward) on F[0], F[m], F[2m], F[3m].
+template <bool FMA = false>
 __device__ __forceinline__ void bfly4(cf& f0, cf& f1, cf& f2, cf& f3, cf w1, cf w2, cf w3) {
-  const cf s0 = cmul(f1, w1);
-  const cf s1 = cmul(f2, w2);
-  const cf s2 = cmul(f3, w3);
+  const cf s0 = cmul_t<FMA>(f1, w1);
+  const cf s1 = cmul_t<FMA>(f2, w2);
+  const cf s2 = cmul_t<FMA>(f3, w3);
   const cf s5 = csub(f0, s1);
   const cf a0 = cadd(f0, s1);
   const cf s3 = cadd(s0, s2);
@@ -74,8 +85,9 @@ __device__ __forceinline__ void bfly2_unit(cf& f0, cf& f1) {
 }
 
 // kissfft.hh:155-162 kf_bfly2 (forward).
+template <bool FMA = false>
 __device__ __forceinline__ void bfly2(cf& f0, cf& f1, cf w) {
-  const cf t = cmul(f1, w);
+  const cf t = cmul_t<FMA>(f1, w);
   const cf a = f0;
   f1 = csub(a, t);
   f0 = cadd(a, t);
