@@ -299,7 +299,7 @@ __device__ __forceinline__ void sym_base(int s, int step, int64_t frame_len, int
 // and apply what precedes the rotation: KIND 0 raw (API estimate, phy.cpp:91-99),
 // KIND 1 LEGACY (caller dechirp, e2e_chain_test.cpp:88-93, then normalisation,
 // LoRaDemod.cpp:68-77), KIND 2 API down-chirp (phy.cpp:216-225).
-template <int SF, int ABL, bool FMA = false>
+template <int SF, int ABL>
 __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restrict__ x, int l,
                                               int osr, int step, int cg, int kind, bool dech,
                                               float scale, cf* in) {
@@ -329,7 +329,7 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
         for (int q = 0; q < P; ++q) in[q] = cmul(in[q], d0);
       } else {
 #pragma unroll
-        for (int q = 0; q < P; ++q) in[q] = cmul_t<FMA>(in[q], dl[(T * q) * osr]);
+        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[(T * q) * osr]);
       }
     }
 #pragma unroll
@@ -614,10 +614,12 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   const float scale = (legacy && p.scaled) ? p.scale : 1.0f;
 
   // The speculative demod with the hardware rotation (certified for every frame) also
-  // uses fused multiply-adds for its complex products, and skips the unit scale.
+  // uses fused multiply-adds for the rotation and the FFT, and skips the unit scale.  The
+  // dechirp product keeps the reference's arithmetic: the frame maximum (hence the scale,
+  // cfo, time_offset and max_amp outputs) is taken over exactly these samples.
   constexpr bool FMA = SPEC && FAST;
   cf in[P], z[P];
-  gather_points<SF, ABL, FMA>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
+  gather_points<SF, ABL>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
   float pm = 0.0f;
   if constexpr (SPEC && !LORA_SPEC_ABL) {  // the window's dechirped, unscaled samples (scale is 1 here)
 #pragma unroll

@@ -260,3 +260,52 @@ def test_fast_precision_rescaled_frames_are_exact(O, amd, sf, snr_db):
         assert int(res.sync[f]) == osync
         assert bits(res.cfo[f].item()) == bits(ocfo)
         assert bits(res.time_offset[f].item()) == bits(otoff)
+
+
+@pytest.mark.parametrize("path", ["hw", "glibc", "split"])
+@pytest.mark.parametrize("sf,dechirp", [(7, True), (7, False), (9, True), (12, True)])
+def test_max_amp_is_the_reference_frame_maximum(O, amd, sf, dechirp, path):
+    """max_amp (LoRaDemod.cpp:59-67: max of |I|, |Q| over the whole frame as handed to
+    lora_demodulate, i.e. after the caller's dechirp) bit for bit, with the rescaling it
+    drives: the pipeline assembles it from window maxima of exactly-dechirped samples (the
+    demod's fused multiply-adds must not reach them).  Frames of random symbols at random
+    amplitude around 1, some with a ragged tail."""
+    import os
+
+    N = 1 << sf
+    S = 6 if sf < 12 else 4
+    F = 48 if sf < 12 else 8
+    rng = np.random.default_rng(4242 + sf + dechirp)
+    L = S * N + 29
+    iq = np.zeros((F, L), np.complex64)
+    for f in range(F):
+        syms = rng.integers(0, N, S - 2).astype(np.uint16)
+        x = O.lora_modulate(syms, sf, 1, 125000, 1.0, int(rng.integers(0, 256)))[: S * N]
+        x = x * np.float32(rng.uniform(0.6, 1.6))
+        x = x + np.float32(0.2) * (rng.standard_normal(S * N) + 1j * rng.standard_normal(S * N))
+        if not dechirp:
+            x = O.dechirp(x.astype(np.complex64), sf, 1)
+        iq[f, : S * N] = x.astype(np.complex64)
+        iq[f, S * N:] = (0.3 * rng.standard_normal(L - S * N)).astype(np.complex64)
+    if path == "split":
+        os.environ["LORA_MI355X_SPEC"] = "0"
+    if path == "glibc":
+        os.environ["LORA_MI355X_SPEC_HW"] = "0"
+    try:
+        plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=dechirp)
+    finally:
+        os.environ.pop("LORA_MI355X_SPEC", None)
+        os.environ.pop("LORA_MI355X_SPEC_HW", None)
+    res = plan.run(torch.from_numpy(iq).cuda())
+    torch.cuda.synchronize()
+    assert ("spec" in plan.last_kernels()) == (path != "split")
+    got = res.max_amp.cpu().numpy()
+    syms = res.symbols.cpu().numpy()
+    for f in range(F):
+        xd = O.dechirp(iq[f], sf, 1) if dechirp else iq[f]
+        ref = np.abs(xd.view(np.float32)).max()
+        assert bits(got[f]) == bits(ref), f"frame {f}: max_amp {got[f]!r} vs {ref!r}"
+        osym, osync, ocfo, otoff = O.lora_demodulate(xd, sf, 1, False)
+        np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
+        assert bits(res.cfo[f].item()) == bits(ocfo)
+        assert bits(res.time_offset[f].item()) == bits(otoff)
