@@ -32,11 +32,9 @@ namespace {
 // chip (tools/micro/pk_rate) and need operand-pairing moves, so for these VALU-bound
 // kernels the scalar forms are cheaper (measured: SF7 demod -7 %, SF12 demod -13 %;
 // tools/exp/variant_ab.sh).  Same IEEE operations either way, so results are unchanged.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define LORA_SCALAR_FP32 __attribute__((target("no-packed-fp32-ops")))
-#else
-#define LORA_SCALAR_FP32  // a device code-generation attribute; nothing on the host pass
-#endif
+// The Makefile drops the packed-fp32-ops feature for this whole translation unit (a
+// per-kernel target attribute kept every non-force-inlined helper out of line).
+#define LORA_SCALAR_FP32
 
 template <int SF>
 struct Geo {
@@ -212,8 +210,14 @@ __device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__
 #ifndef LORA_SPEC_ABL
 #define LORA_SPEC_ABL 0  // A/B only: 1 = skip the speculative extras (results invalid)
 #endif
+#ifndef LORA_SPEC_ABLX
+#define LORA_SPEC_ABLX 0  // A/B only: ablation bits (ABL below) for the speculative demod
+#endif
 
-template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false>
+// XA: profiling-only ablation bits of the speculative kernel (LORA_SPEC_ABLX, results
+// invalid): 16 = no LDS reads (the lane's own values stand in), 32 = one twiddle load
+// per group instead of one per butterfly input.
+template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false, int XA = 0>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
                                          uint64_t& key, const cf* __restrict__ twT = nullptr,
                                          float* second = nullptr) {
@@ -224,8 +228,20 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     const int k = GI % MA, cc = GI / MA;
     cf* xs = x + gg * R;
     const cf* rb = row + lds_slot<SF>(cc * MA * R + k);  // k < MA, MA*u: disjoint bits
+    if constexpr (!(XA & 16)) {
 #pragma unroll
-    for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
+      for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
+    }
+    if constexpr ((XA & 32) && (R == 4 || R == 16)) {
+      const cf w = twT ? twT[k] : tw[k];
+#pragma unroll
+      for (int blk = 0; blk < R; blk += 4) bfly4<FMA>(xs[blk], xs[blk + 1], xs[blk + 2], xs[blk + 3], w, w, w);
+      if constexpr (R == 16) {
+#pragma unroll
+        for (int uu = 0; uu < 4; ++uu) bfly4<FMA>(xs[uu], xs[uu + 4], xs[uu + 8], xs[uu + 12], w, w, w);
+      }
+      continue;
+    }
     if constexpr (R == 4 || R == 16) {
       if (twT) {
         pass_regs_T<R, MA, FMA>(xs, k, twT);
@@ -432,18 +448,22 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
 #pragma unroll
     for (int h = 0; h < G::G1; ++h)
 #pragma unroll
-      for (int u = 0; u < R1; ++u) row[lds_slot<SF>(c[h] * R1) + u] = z[h * R1 + u];  // u < 16
-    block_sync<WL>();
+      for (int u = 0; u < R1; ++u)
+        if (!(ABL & 16)) row[lds_slot<SF>(c[h] * R1) + u] = z[h * R1 + u];  // u < 16
+    if (!(ABL & 16)) block_sync<WL>();
     constexpr int RL = G::NPASS == 2 ? G::RA : G::RB;   // last pass span
     constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
+    constexpr int XA = ABL & 48;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA>(row, z, l, a.tw, key, a.twTA, second);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA, XA>(row, z, l, a.tw, key, a.twTA, second);
     } else {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA>(row, z, l, a.tw, key, a.twTA);
-      block_sync<WL>();
-      write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
-      block_sync<WL>();
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA>(row, z, l, a.tw, key, a.twTB, second);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA, XA>(row, z, l, a.tw, key, a.twTA);
+      if (!(ABL & 16)) {
+        block_sync<WL>();
+        write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
+        block_sync<WL>();
+      }
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, XA>(row, z, l, a.tw, key, a.twTB, second);
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)
@@ -586,6 +606,7 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
   constexpr bool RAW = MODE == 3;
   constexpr bool DYN = MODE >= 2;
+  constexpr int AB = ABL | (SPEC ? LORA_SPEC_ABLX : 0);  // profiling-only ablation bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint64_t red[4];
   cf* rows = reinterpret_cast<cf*>(smem);
@@ -619,17 +640,17 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   // cfo, time_offset and max_amp outputs) is taken over exactly these samples.
   constexpr bool FMA = SPEC && FAST;
   cf in[P], z[P];
-  gather_points<SF, ABL>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
+  gather_points<SF, AB>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
   float pm = 0.0f;
   if constexpr (SPEC && !LORA_SPEC_ABL) {  // the window's dechirped, unscaled samples (scale is 1 here)
 #pragma unroll
     for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
   }
-  rotate_place<SF, !RAW, ABL, FAST, FMA>(in, z, start, p.rate, hann, a.win, l);
+  rotate_place<SF, !RAW, AB, FAST, FMA>(in, z, start, p.rate, hann, a.win, l);
   if constexpr (SPEC && !LORA_SPEC_ABL) asm volatile("" : "+v"(pm));
   float sec = 0.0f;
   const uint64_t lkey =
-      fft_key<SF, false, ABL, FMA>(z, rows + (size_t)g * rowc, l, a, SPEC && !LORA_SPEC_ABL ? &sec : nullptr);
+      fft_key<SF, false, AB, FMA>(z, rows + (size_t)g * rowc, l, a, SPEC && !LORA_SPEC_ABL ? &sec : nullptr);
   const uint64_t key = symbol_key<SF>(lkey, tid, red);
   if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + (s - s0)] = (uint16_t)key_index(key);
   if constexpr (SPEC && !LORA_SPEC_ABL) {
@@ -1414,6 +1435,618 @@ bool launch_fused_sf(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t
                    : launch_fused_mode<SF, 1, false>(a, frames, lds_max, st);
 }
 
+// ---- streaming speculative demod (SF 7-10: a symbol within one wave) -----------------
+// The speculative symbol pass as a persistent kernel that keeps the next symbol group's
+// IQ in flight while it transforms the current one.  Ablations of k_demod_fast<SPEC>
+// (tools/exp/spec_ablate.sh) put 42 % of its time on the IQ gathers: at the 4-waves/SIMD
+// ceiling its waves issue their loads and then wait, and every dechirp-table and twiddle
+// load after them waits too (vmcnt retires in order).  Here:
+//   * one workgroup of 8 waves per CU walks the symbol groups (64/T symbols = 1,024
+//     points per wave) in wave-interleaved order;
+//   * each group's windows arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+//     instruction, no VGPR destination): 8 pieces + one dword piece for the last sample
+//     of an odd-aligned window, issued one group AHEAD into the other of two per-wave
+//     buffers, and waited for with a counted vmcnt;
+//   * nothing else in the loop is a vector-memory load: the dechirp table sits in LDS,
+//     the lane's pass twiddles and pass-1 twiddles in registers (loaded once), the frame
+//     offsets come by scalar loads, and the two result stores are counted;
+//   * a group's buffer, once read into registers, is the symbol rows of its transposes.
+// Arithmetic is k_demod_fast<SF, MODE, 0, true, true>'s, operation for operation (the
+// same dechirp, window maximum, hardware rotation with fused multiply-adds, butterflies
+// and twiddle values, margin), so margins, maxima and symbols are identical to it.
+#ifndef LORA_STREAM_ABL
+#define LORA_STREAM_ABL 0  // A/B only (results invalid): 1 = no DMA issued, 2 = no transform, 4 = no dechirp
+#endif
+// Geometry of the streaming kernel: P points per lane, T = N/P lanes per symbol, a wave
+// group of SPWV = 64/T symbols (1,024 or 512 points).  P = 16 is Geo<SF>'s shape; P = 8
+// (SF 7: 16 lanes per symbol) halves a wave's LDS so 16 waves fit a CU: pass 1 radix-2 +
+// radix-4 (stages m = 1, 2), then two radix-4 LDS passes (m = 8, 32) instead of one
+// register-blocked radix-16 pass - kissfft's butterflies, twiddles and order either way.
+template <int SF, int PP>
+struct StreamGeo {
+  static constexpr int N = 1 << SF;
+  static constexpr int P = PP;
+  static constexpr int T = N / P;
+  static constexpr int R1 = (SF & 1) ? 8 : 16;                  // pass-1 span
+  static constexpr int LOGR1 = (SF & 1) ? 3 : 4;
+  static constexpr int G1 = P / R1;
+  static constexpr bool R2FIRST = (SF & 1) != 0;
+  static constexpr int X = N / R1;
+  static constexpr int RA = X >= 16 && P >= 16 ? 16 : 4;         // pass-A span
+  static constexpr int RB = X / RA;                              // pass-B span (1 = none)
+  static constexpr int NPASS = RB > 1 ? 3 : 2;
+  static constexpr int MA_A = R1, MA_B = R1 * RA;
+  static constexpr int SPWV = 64 / T;                            // symbols per wave group
+  static constexpr int ROWC = (lds_row<SF>() + 1) & ~1;          // row stride in complex (16-B multiple)
+  static constexpr int ROWB = ROWC * 8;
+  static constexpr int PIECES = N / 128;                         // 1-KiB DMA pieces per symbol
+  static constexpr int BUFB = SPWV * ROWB;
+  static constexpr int TAILB = 256;                              // 64 lanes x 4 B (last-sample piece)
+  static constexpr int PARB = SPWV * 32;
+  static constexpr int WAVEB = 2 * (BUFB + TAILB + PARB);
+  static constexpr int WAVES = P == 8 ? 16 : 8;                  // waves per workgroup (one per CU)
+  static constexpr int NDMA = SPWV * PIECES + 1;                 // DMA instructions per group
+  static_assert(G1 >= 1 && RB <= 16 && (RB == 1 || RB == 4 || RB == 16) && RA * RB * R1 == N, "pass shape");
+  static_assert(P == 16 || (P == 8 && SF == 7), "P = 8 only for SF 7");
+  static_assert(ROWC >= N + 1, "a row holds the window plus the odd-alignment shift");
+};
+
+// Pass-1 register of point q: (q % G1) * R1 + leaf_pos(R1, q / G1), folded at compile time.
+template <int P, int G1, int R1>
+struct ZIdx {
+  int v[P];
+};
+template <int P, int G1, int R1>
+constexpr ZIdx<P, G1, R1> make_zidx() {
+  ZIdx<P, G1, R1> z{};
+  for (int q = 0; q < P; ++q) z.v[q] = (q % G1) * R1 + leaf_pos(R1, q / G1);
+  return z;
+}
+
+// group_reduce2 for groups of T <= 64 lanes (wave-local)
+template <int T>
+__device__ __forceinline__ void group_reduce2_w(float& a, float& b) {
+#pragma unroll
+  for (int o = T >> 1; o > 0; o >>= 1) {
+    a = fmaxf(a, __shfl_xor(a, o, 64));
+    b = fmaxf(b, __shfl_xor(b, o, 64));
+  }
+}
+
+struct StreamSym {  // one symbol of a group (LDS, written when its DMA is issued)
+  float start, rate;
+  int cg, shift;
+  int64_t marg_idx, sym_idx;
+};
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)p; }
+
+// LDS-DMA: each lane's 16 (4) bytes at g land at LDS byte lds + lane*16 (lane*4).  M0 is
+// written and restored inside the statement (cdna_hip_programming.md, LDS-DMA recipe);
+// hipcc does not count these loads, the kernel waits for them itself.
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+__device__ __forceinline__ void dma16(const void* g, uint32_t lds) {
+  unsigned keep;
+  lds = __builtin_amdgcn_readfirstlane(lds);
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds)
+               : "memory");
+}
+__device__ __forceinline__ void dma4(const void* g, uint32_t lds) {
+  unsigned keep;
+  lds = __builtin_amdgcn_readfirstlane(lds);
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds)
+               : "memory");
+}
+// Frame offsets by scalar loads (wave-uniform frame): rate (+8) and t_off (+16).
+__device__ __forceinline__ void sload_fp(const FrameParams* p, float& rate, int& t_off) {
+  uint32_t r, t;
+  p = reinterpret_cast<const FrameParams*>(rfl64(reinterpret_cast<uint64_t>(p)));
+  asm volatile("s_load_dword %0, %2, 0x8\n\ts_load_dword %1, %2, 0x10\n\ts_waitcnt lgkmcnt(0)"
+               : "=&s"(r), "=&s"(t)
+               : "s"(p)
+               : "memory");
+  rate = __uint_as_float(r);
+  t_off = (int)t;
+}
+__device__ __forceinline__ void store_u16(uint16_t* p, uint32_t v) {
+  asm volatile("global_store_short %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void store_f2(float2* p, float2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+
+// Issue group g's windows into buffer `buf` (wave-uniform LDS byte address) and record
+// each symbol's parameters in `par`.  Symbols past `work` mirror the last one (identical
+// values to identical addresses).  All control flow is wave-uniform.
+template <int SF, int PP>
+__device__ __forceinline__ void stream_issue(const KArgs& a, int g, int work, int per, uint32_t buf,
+                                             uint32_t tail, StreamSym* par, int lane) {
+  using SG = StreamGeo<SF, PP>;
+  constexpr int N = SG::N, SPWV = SG::SPWV;
+  const int w0 = g * SPWV;
+  int wc = w0 < work ? w0 : work - 1;
+  int f = wc / per, r = wc - f * per;
+  const char* tsrc = nullptr;
+#pragma unroll
+  for (int j = 0; j < SPWV; ++j) {
+    if (j > 0 && w0 + j < work) {
+      ++wc;
+      if (++r == per) {
+        r = 0;
+        ++f;
+      }
+    }
+    float rate;
+    int t_off;
+    sload_fp(a.fp_spec + f, rate, t_off);
+    const int s = 2 + r;
+    int64_t base;
+    int cg;
+    sym_base(s, N, a.frame_len, t_off, base, cg);
+    const char* B = reinterpret_cast<const char*>(a.iq + (int64_t)f * a.frame_stride + base);
+    const int shift = (int)(((uintptr_t)B >> 3) & 1);
+    const char* A = B - 8 * shift;  // 16-B aligned (frames start 16-B aligned)
+#pragma unroll
+    for (int c = 0; c < SG::PIECES; ++c)
+      if (!(LORA_STREAM_ABL & 1)) dma16(A + c * 1024 + lane * 16, buf + j * SG::ROWB + c * 1024);
+    if (((lane >> 1) % SPWV) == j) tsrc = B + 8 * (N - 1) + 4 * (lane & 1);
+    if (lane == 0) {
+      StreamSym sp;
+      sp.start = rate * ((float)((uint32_t)s * (uint32_t)N) + (float)t_off);  // osr 1
+      sp.rate = rate;
+      sp.cg = cg;
+      sp.shift = shift;
+      sp.marg_idx = wc;
+      sp.sym_idx = (int64_t)f * a.sym_stride + r;
+      par[j] = sp;
+    }
+  }
+  if (!(LORA_STREAM_ABL & 1)) dma4(tsrc, tail);
+}
+
+// pass_lds with the lane's twiddles in registers: w[gg * (R == 16 ? 15 : 3) + j] =
+// twT[j * MA + k] of group gg (lora::twT_index), same butterflies and order.
+template <int R, int MA, int SF, int T, int P, bool LAST>
+__device__ __forceinline__ void pass_lds_rw(cf* row, cf* x, int l, const cf* w, uint64_t& key, float* second) {
+  constexpr int NG = P / R, NT = R == 16 ? 15 : 3;
+#pragma unroll
+  for (int gg = 0; gg < NG; ++gg) {
+    const int GI = l + T * gg;
+    const int k = GI % MA, cc = GI / MA;
+    cf* xs = x + gg * R;
+    const cf* rb = row + lds_slot<SF>(cc * MA * R + k);
+#pragma unroll
+    for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
+    const cf* wg = w + gg * NT;
+#pragma unroll
+    for (int blk = 0; blk < R; blk += 4) bfly4<true>(xs[blk], xs[blk + 1], xs[blk + 2], xs[blk + 3], wg[0], wg[1], wg[2]);
+    if constexpr (R == 16) {
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu)
+        bfly4<true>(xs[uu], xs[uu + 4], xs[uu + 8], xs[uu + 12], wg[3 + 3 * uu], wg[4 + 3 * uu], wg[5 + 3 * uu]);
+    }
+  }
+  if constexpr (LAST) {
+    float best = 0.0f, sec = 0.0f;
+    uint32_t bi = (uint32_t)l;
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int gg = 0; gg < NG; ++gg) {
+        const cf v = x[gg * R + u];
+        const float m2 = v.re * v.re + v.im * v.im;
+        const uint32_t bin = (uint32_t)(l + T * gg + MA * u);
+        sec = __builtin_amdgcn_fmed3f(sec, m2, best);
+        if (m2 > best) {
+          best = m2;
+          bi = bin;
+        }
+      }
+    key = ((uint64_t)__float_as_uint(best) << 32) | (uint32_t)(~bi);
+    *second = sec;
+  }
+}
+
+// pass_regs<R, R2, N, 1, UNIT = true, FMA = true>(x, 0, tw) with tw[m * N / R] = t1[m].
+template <int R, bool R2>
+__device__ __forceinline__ void pass1_rw(cf* x, const cf* t1) {
+  int S = 1;
+  if constexpr (R2) {
+#pragma unroll
+    for (int b = 0; b < R; b += 2) bfly2_unit(x[b], x[b + 1]);
+    S = 2;
+  }
+#pragma unroll
+  for (; S < R; S *= 4) {
+    const int ms = R / (4 * S);  // tw index q*uu*fs, fs = N/(4S) = ms * (N/R)
+#pragma unroll
+    for (int blk = 0; blk < R; blk += 4 * S) {
+#pragma unroll
+      for (int uu = 0; uu < S; ++uu) {
+        if (uu == 0)
+          bfly4_unit(x[blk], x[blk + S], x[blk + 2 * S], x[blk + 3 * S]);
+        else
+          bfly4<true>(x[blk + uu], x[blk + uu + S], x[blk + uu + 2 * S], x[blk + uu + 3 * S], t1[uu * ms],
+                      t1[2 * uu * ms], t1[3 * uu * ms]);
+      }
+    }
+  }
+}
+
+template <int SF, int MODE, int PP>
+__global__ void __launch_bounds__((StreamGeo<SF, PP>::WAVES * 64))
+__attribute__((amdgpu_waves_per_eu(StreamGeo<SF, PP>::WAVES / 4)))
+LORA_SCALAR_FP32 k_demod_stream(KArgs a, int work, int ngroups) {
+  using SG = StreamGeo<SF, PP>;
+  constexpr int N = SG::N, T = SG::T, P = SG::P, R1 = SG::R1, SPWV = SG::SPWV, NT = SG::WAVES * 64;
+  constexpr int NGA = P / SG::RA, NGB = SG::NPASS == 3 ? P / SG::RB : 0;
+  constexpr int NTA = SG::RA == 16 ? 15 : 3, NTB = SG::RB == 16 ? 15 : 3;
+  constexpr int TABB = MODE == 0 ? 2 * N * 8 : 0;
+  constexpr ZIdx<P, SG::G1, R1> ZI = make_zidx<P, SG::G1, R1>();
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cf* dtab = reinterpret_cast<cf*>(smem);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int per = a.total - 2;
+
+  // ---- prologue: dechirp table to LDS, the lane's twiddles and digit-reverse rows ----
+  if constexpr (MODE == 0)
+    for (int i = tid; i < 2 * N; i += NT) dtab[i] = a.down[i];
+  const int l = lane % T, j = lane / T;
+  cf t1[12];
+#pragma unroll
+  for (int m = 0; m < 12; ++m) t1[m] = (m * (N / R1) < N) ? a.tw[m * (N / R1)] : cf{0.0f, 0.0f};
+  // the lane's pass twiddles, read from the natural table at the slot-major copy's
+  // indices (lora::twT_index; the copy, when the plan has one, holds the same values)
+  cf twA[NGA * NTA];
+#pragma unroll
+  for (int gg = 0; gg < NGA; ++gg)
+#pragma unroll
+    for (int jj = 0; jj < NTA; ++jj) twA[gg * NTA + jj] = a.tw[twT_index(N, SG::MA_A, jj, (l + T * gg) % SG::MA_A)];
+  cf twB[NGB > 0 ? NGB * NTB : 1];
+  if constexpr (NGB > 0) {
+#pragma unroll
+    for (int gg = 0; gg < NGB; ++gg)
+#pragma unroll
+      for (int jj = 0; jj < NTB; ++jj) twB[gg * NTB + jj] = a.tw[twT_index(N, SG::MA_B, jj, (l + T * gg) % SG::MA_B)];
+  }
+  int c[SG::G1];
+#pragma unroll
+  for (int h = 0; h < SG::G1; ++h) c[h] = (int)(a.rev[l + T * h] >> SG::LOGR1);
+  // settle every prologue load here: no compiler-counted vector load may remain pending
+  // inside the loop (its wait would also drain the DMA in flight)
+#pragma unroll
+  for (int m = 0; m < 12; ++m) asm volatile("" : "+v"(t1[m].re), "+v"(t1[m].im));
+#pragma unroll
+  for (int m = 0; m < NGA * NTA; ++m) asm volatile("" : "+v"(twA[m].re), "+v"(twA[m].im));
+  if constexpr (NGB > 0) {
+#pragma unroll
+    for (int m = 0; m < NGB * NTB; ++m) asm volatile("" : "+v"(twB[m].re), "+v"(twB[m].im));
+  }
+#pragma unroll
+  for (int h = 0; h < SG::G1; ++h) asm volatile("" : "+v"(c[h]));
+  __syncthreads();
+
+  unsigned char* wbase = smem + TABB + wave * SG::WAVEB;
+  auto bufp = [&](int b) { return wbase + b * SG::BUFB; };
+  auto tailp = [&](int b) { return wbase + 2 * SG::BUFB + b * SG::TAILB; };
+  auto parp = [&](int b) { return reinterpret_cast<StreamSym*>(wbase + 2 * (SG::BUFB + SG::TAILB) + b * SG::PARB); };
+
+  const int NW = gridDim.x * SG::WAVES;
+  int g = blockIdx.x * SG::WAVES + wave;
+  if (g < ngroups) stream_issue<SF, PP>(a, g, work, per, lds_u32(bufp(0)), lds_u32(tailp(0)), parp(0), lane);
+  for (int it = 0; g < ngroups; ++it, g += NW) {
+    const int nb = it & 1;
+    const bool more = g + NW < ngroups;
+    if (more) stream_issue<SF, PP>(a, g + NW, work, per, lds_u32(bufp(nb ^ 1)), lds_u32(tailp(nb ^ 1)), parp(nb ^ 1), lane);
+    // group g's pieces landed: younger are the previous group's 2 stores (it > 0) and the
+    // next group's NDMA pieces (more); vmcnt retires in issue order
+    if (it > 0) {
+      if (more)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SG::NDMA + 2) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      if (more)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SG::NDMA) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const StreamSym sp = parp(nb)[j];
+    cf* row = reinterpret_cast<cf*>(bufp(nb) + j * SG::ROWB);
+    const cf* src = row + sp.shift + l;
+    cf in[P], z[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) in[q] = src[T * q];
+    {  // the window's last sample of an odd-aligned window came in the dword piece
+      const cf tv = reinterpret_cast<const cf*>(tailp(nb))[j];
+      if (l == T - 1 && sp.shift) in[P - 1] = tv;
+    }
+    wave_sync();  // every lane's samples are in registers before the row is reused
+    if constexpr (LORA_STREAM_ABL & 2) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int q = 0; q < P; ++q) acc = amax3(acc, in[q]);
+      store_u16(a.syms + sp.sym_idx, __float_as_uint(acc) & 0xFFFFu);
+      store_f2(reinterpret_cast<float2*>(a.spec_marg) + sp.marg_idx, make_float2(acc, acc));
+      continue;
+    }
+    if constexpr (MODE == 0 && !(LORA_STREAM_ABL & 4)) {
+      const cf* dl = dtab + sp.cg + l;
+#pragma unroll
+      for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[T * q]);
+    }
+    float pm = 0.0f;
+#pragma unroll
+    for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
+    {
+      constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const float ph = sp.start + sp.rate * (float)(l + T * q);
+        const float rev = __builtin_amdgcn_fractf(ph * INV_2PI);
+        z[ZI.v[q]] =
+            cmul_t<true>(in[q], cf{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)});
+      }
+    }
+    asm volatile("" : "+v"(pm));
+#pragma unroll
+    for (int h = 0; h < SG::G1; ++h) pass1_rw<R1, SG::R2FIRST>(z + h * R1, t1);
+#pragma unroll
+    for (int h = 0; h < SG::G1; ++h)
+#pragma unroll
+      for (int u = 0; u < R1; ++u) row[lds_slot<SF>(c[h] * R1) + u] = z[h * R1 + u];
+    wave_sync();
+    uint64_t lkey = 0;
+    float sec = 0.0f;
+    if constexpr (SG::NPASS == 2) {
+      pass_lds_rw<SG::RA, SG::MA_A, SF, T, P, true>(row, z, l, twA, lkey, &sec);
+    } else {
+      pass_lds_rw<SG::RA, SG::MA_A, SF, T, P, false>(row, z, l, twA, lkey, &sec);
+      wave_sync();
+      write_pass<SG::RA, SG::MA_A, SF, T, P>(row, z, l);
+      wave_sync();
+      pass_lds_rw<SG::RB, SG::MA_B, SF, T, P, true>(row, z, l, twB, lkey, &sec);
+    }
+    const uint64_t key = group_max(lkey, T);
+    float r2 = lkey == key ? sec : key_value(lkey);
+    group_reduce2_w<T>(r2, pm);
+    // every lane of the symbol stores the symbol's (identical) results: 2 full-wave stores
+    store_u16(a.syms + sp.sym_idx, key_index(key) & 0xFFFFu);
+    store_f2(reinterpret_cast<float2*>(a.spec_marg) + sp.marg_idx, make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm));
+  }
+}
+
+template <int SF, int MODE, int PP>
+bool launch_stream(const KArgs& a, int64_t work, hipStream_t st) {
+  using SG = StreamGeo<SF, PP>;
+  constexpr int TABB = MODE == 0 ? 2 * (1 << SF) * 8 : 0;
+  const size_t lds = TABB + SG::WAVES * SG::WAVEB;
+  static_assert(TABB + SG::WAVES * SG::WAVEB <= 160 * 1024, "LDS budget");
+  if (work <= 0 || work >= (int64_t(1) << 31) || !a.syms || !a.spec_marg || !a.fp_spec || !a.tw || !a.rev ||
+      (MODE == 0 && !a.down) || a.total < 3)
+    return false;
+  // frames start 16-byte aligned, so a window's 16-B aligned superset stays in its frame
+  if ((a.frame_stride & 1) || (reinterpret_cast<uintptr_t>(a.iq) & 15)) return false;
+  static int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  if (hipFuncSetAttribute((const void*)k_demod_stream<SF, MODE, PP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return false;
+  const int ngroups = (int)((work + SG::SPWV - 1) / SG::SPWV);
+  const int grid = std::max(1, std::min(ncu, (ngroups + SG::WAVES - 1) / SG::WAVES));
+  hipLaunchKernelGGL((k_demod_stream<SF, MODE, PP>), dim3((unsigned)grid), dim3(SG::WAVES * 64), lds, st, a, (int)work,
+                     ngroups);
+  return true;
+}
+
+// ---- register-prefetch speculative demod (SF 7) ---------------------------------------
+// The streaming kernel's alternative without LDS-DMA: persistent 4-wave workgroups at
+// 4 waves/SIMD, P = 8 points per lane (StreamGeo<7, 8>: 16 lanes per symbol, 4 symbols
+// per wave group), and the next group's samples loaded into registers (8 x 8 B per lane)
+// before the current group is transformed.  No other vector-memory load is in the loop
+// (dechirp table: registers for the common phase 0, else LDS; twiddles: registers), so
+// hipcc's own vmcnt bookkeeping waits for exactly the prefetch when its values are used.
+// Same arithmetic as k_demod_fast<7, MODE, 0, true, true>.
+#ifndef LORA_PF_DREG
+#define LORA_PF_DREG 1  // keep the phase-0 dechirp values of the lane in registers
+#endif
+struct PfSym {
+  const cf* x;  // the lane's first sample of its window
+  float start, rate;
+  int cg, marg_idx;
+  int64_t sym_idx;
+};
+
+template <int SF>
+__device__ __forceinline__ PfSym pf_params(const KArgs& a, int g, int work, int per, int lane) {
+  using SG = StreamGeo<SF, 8>;
+  constexpr int N = SG::N, T = SG::T, SPWV = SG::SPWV;
+  const int w0 = g * SPWV;
+  int wc = w0 < work ? w0 : work - 1;
+  int f = wc / per, r = wc - f * per;
+  PfSym me{};
+  const int jl = lane / T, l = lane % T;
+#pragma unroll
+  for (int j = 0; j < SPWV; ++j) {
+    if (j > 0 && w0 + j < work) {
+      ++wc;
+      if (++r == per) {
+        r = 0;
+        ++f;
+      }
+    }
+    float rate;
+    int t_off;
+    sload_fp(a.fp_spec + f, rate, t_off);
+    const int s = 2 + r;
+    int64_t base;
+    int cg;
+    sym_base(s, N, a.frame_len, t_off, base, cg);
+    if (jl == j) {
+      me.x = a.iq + (int64_t)f * a.frame_stride + base + l;
+      me.start = rate * ((float)((uint32_t)s * (uint32_t)N) + (float)t_off);  // osr 1
+      me.rate = rate;
+      me.cg = cg;
+      me.marg_idx = wc;
+      me.sym_idx = (int64_t)f * a.sym_stride + r;
+    }
+  }
+  return me;
+}
+
+template <int SF, int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+LORA_SCALAR_FP32 k_demod_pf(KArgs a, int work, int ngroups) {
+  using SG = StreamGeo<SF, 8>;
+  constexpr int N = SG::N, T = SG::T, P = SG::P, R1 = SG::R1;
+  constexpr int NGA = P / SG::RA, NGB = SG::NPASS == 3 ? P / SG::RB : 0;
+  constexpr int NTA = SG::RA == 16 ? 15 : 3, NTB = SG::RB == 16 ? 15 : 3;
+  constexpr int TABB = MODE == 0 ? 2 * N * 8 : 0;
+  constexpr ZIdx<P, SG::G1, R1> ZI = make_zidx<P, SG::G1, R1>();
+  static_assert(SG::NPASS == 3, "two LDS passes");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cf* dtab = reinterpret_cast<cf*>(smem);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int per = a.total - 2;
+  const int l = lane % T, j = lane / T;
+
+  if constexpr (MODE == 0)
+    for (int i = tid; i < 2 * N; i += 256) dtab[i] = a.down[i];
+  cf t1[12];
+#pragma unroll
+  for (int m = 0; m < 12; ++m) t1[m] = (m * (N / R1) < N) ? a.tw[m * (N / R1)] : cf{0.0f, 0.0f};
+  cf twA[NGA * NTA], twB[NGB * NTB];
+#pragma unroll
+  for (int gg = 0; gg < NGA; ++gg)
+#pragma unroll
+    for (int jj = 0; jj < NTA; ++jj) twA[gg * NTA + jj] = a.tw[twT_index(N, SG::MA_A, jj, (l + T * gg) % SG::MA_A)];
+#pragma unroll
+  for (int gg = 0; gg < NGB; ++gg)
+#pragma unroll
+    for (int jj = 0; jj < NTB; ++jj) twB[gg * NTB + jj] = a.tw[twT_index(N, SG::MA_B, jj, (l + T * gg) % SG::MA_B)];
+  int c0 = (int)(a.rev[l] >> SG::LOGR1);
+  cf dreg[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) dreg[q] = (MODE == 0 && LORA_PF_DREG) ? a.down[l + T * q] : cf{0.0f, 0.0f};
+  // settle every prologue load here (a load still pending at the loop would be waited
+  // for inside it, behind the prefetch)
+#pragma unroll
+  for (int m = 0; m < 12; ++m) asm volatile("" : "+v"(t1[m].re), "+v"(t1[m].im));
+#pragma unroll
+  for (int m = 0; m < NGA * NTA; ++m) asm volatile("" : "+v"(twA[m].re), "+v"(twA[m].im));
+#pragma unroll
+  for (int m = 0; m < NGB * NTB; ++m) asm volatile("" : "+v"(twB[m].re), "+v"(twB[m].im));
+#pragma unroll
+  for (int q = 0; q < P; ++q) asm volatile("" : "+v"(dreg[q].re), "+v"(dreg[q].im));
+  asm volatile("" : "+v"(c0));
+  __syncthreads();
+
+  const int NW = gridDim.x * 4;
+  int g = blockIdx.x * 4 + wave;
+  if (g >= ngroups) return;
+  cf* row = reinterpret_cast<cf*>(smem + TABB + (wave * SG::SPWV + j) * SG::ROWB);
+  PfSym nxt = pf_params<SF>(a, g, work, per, lane);
+  cf nin[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) nin[q] = nxt.x[T * q];
+  for (;;) {
+    const PfSym cur = nxt;
+    cf in[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) in[q] = nin[q];
+    // the next group's samples (the last iteration re-reads its own windows, from L2)
+    const int gn = g + NW;
+    const bool more = gn < ngroups;
+    nxt = pf_params<SF>(a, more ? gn : g, work, per, lane);
+#pragma unroll
+    for (int q = 0; q < P; ++q) nin[q] = nxt.x[T * q];
+    if constexpr (MODE == 0) {
+      if (LORA_PF_DREG && __all(cur.cg == 0)) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dreg[q]);
+      } else {
+        const cf* dl = dtab + cur.cg + l;
+#pragma unroll
+        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[T * q]);
+      }
+    }
+    float pm = 0.0f;
+#pragma unroll
+    for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
+    cf z[P];
+    {
+      constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const float ph = cur.start + cur.rate * (float)(l + T * q);
+        const float rev = __builtin_amdgcn_fractf(ph * INV_2PI);
+        z[ZI.v[q]] = cmul_t<true>(in[q], cf{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)});
+      }
+    }
+    asm volatile("" : "+v"(pm));
+    pass1_rw<R1, SG::R2FIRST>(z, t1);
+#pragma unroll
+    for (int u = 0; u < R1; ++u) row[lds_slot<SF>(c0 * R1) + u] = z[u];
+    wave_sync();
+    uint64_t lkey = 0;
+    float sec = 0.0f;
+    pass_lds_rw<SG::RA, SG::MA_A, SF, T, P, false>(row, z, l, twA, lkey, &sec);
+    wave_sync();
+    write_pass<SG::RA, SG::MA_A, SF, T, P>(row, z, l);
+    wave_sync();
+    pass_lds_rw<SG::RB, SG::MA_B, SF, T, P, true>(row, z, l, twB, lkey, &sec);
+    const uint64_t key = group_max(lkey, T);
+    float r2 = lkey == key ? sec : key_value(lkey);
+    group_reduce2_w<T>(r2, pm);
+    if (l == 0) {
+      a.syms[cur.sym_idx] = (uint16_t)key_index(key);
+      reinterpret_cast<float2*>(a.spec_marg)[cur.marg_idx] = make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm);
+    }
+    wave_sync();  // the row's last reads before the next group's write-back
+    if (!more) break;
+    g = gn;
+  }
+}
+
+template <int SF, int MODE>
+bool launch_pf(const KArgs& a, int64_t work, hipStream_t st) {
+  using SG = StreamGeo<SF, 8>;
+  constexpr int TABB = MODE == 0 ? 2 * (1 << SF) * 8 : 0;
+  const size_t lds = TABB + 4 * SG::SPWV * SG::ROWB;
+  if (work <= 0 || work >= (int64_t(1) << 31) || !a.syms || !a.spec_marg || !a.fp_spec || !a.tw || !a.rev ||
+      (MODE == 0 && !a.down) || a.total < 3)
+    return false;
+  static int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  static int per_cu = [] {
+    const char* e = std::getenv("LORA_MI355X_PF_WG");  // A/B knob: workgroups per CU
+    return e ? std::max(1, std::atoi(e)) : 4;
+  }();
+  const int ngroups = (int)((work + SG::SPWV - 1) / SG::SPWV);
+  const int grid = std::max(1, std::min(ncu * per_cu, (ngroups + 3) / 4));
+  hipLaunchKernelGGL((k_demod_pf<SF, MODE>), dim3((unsigned)grid), dim3(256), lds, st, a, (int)work, ngroups);
+  return true;
+}
+
 template <int SF>
 int row_complex() {
   return lds_row<SF>();
@@ -1470,6 +2103,26 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
     const int64_t work = frames * (int64_t)(a.total - 2);
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
     if (stage == 1) {
+      if constexpr (SF >= 7 && SF <= 10) {
+        // LORA_MI355X_STREAM (A/B, opt-in): "1" = SF 7 (P = 8), "all" = SF 7-10, unset/"0" = off
+        static const int stream = [] {
+          const char* e = std::getenv("LORA_MI355X_STREAM");
+          return !e ? 0 : e[0] == '0' ? 0 : (e[0] == 'a' ? 2 : 1);
+        }();
+        constexpr int PP = SF == 7 ? 8 : 16;
+        if constexpr (SF == 7) {
+          static const bool pf = [] {
+            const char* e = std::getenv("LORA_MI355X_PF");
+            return e && e[0] == '1';
+          }();
+          if (pf && (a.fast_rot || a.spec_hw) &&
+              (a.dechirp ? launch_pf<SF, 0>(a, work, st) : launch_pf<SF, 1>(a, work, st)))
+            return true;
+        }
+        if (stream && (SF == 7 || stream == 2) && (a.fast_rot || a.spec_hw) &&
+            (a.dechirp ? launch_stream<SF, 0, PP>(a, work, st) : launch_stream<SF, 1, PP>(a, work, st)))
+          return true;
+      }
       if (a.fast_rot || a.spec_hw)
         return a.dechirp ? launch_mode<SF, 0, 0, true, true>(a, 2, work, st)
                          : launch_mode<SF, 1, 0, true, true>(a, 2, work, st);
