@@ -355,6 +355,9 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 
 // CFO rotation (glibc-faithful sincosf, LoRaDemod.cpp:151-157) when ROT, window
 // (:158-160), and placement in pass-1 leaf order.
+#ifndef LORA_ROT_REC
+#define LORA_ROT_REC 1  // certified demod: rotation factors by recurrence (0: one sin/cos pair per point)
+#endif
 template <int SF, bool ROT, int ABL, bool FAST = false, bool FMA = false>
 __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, float rate,
                                              bool hann, const float* __restrict__ win, int l) {
@@ -365,6 +368,29 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
     // sine/cosine on its fractional revolution (v_fract, v_sin_f32, v_cos_f32) instead of
     // glibc's sincosf - not bit-exact (include/lora_mi355x.h states the tolerance).
     constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
+#if LORA_ROT_REC
+    if constexpr (FMA) {
+      // Certified speculative demod: the lane's points i = l + T*q are T apart, so the
+      // factor of point q is e^{i(ph_l + q*rate*T)}: one hardware sin/cos pair for the
+      // lane's first point, one for the step rate*T (exact in fp32: T is a power of two),
+      // then a fused complex product per point.  Each factor stays within
+      // 4 eps rmax L + 5.4e-6 of the exact one (k_est_fast<SPEC = 2> states the bound and
+      // certifies against the exact reference with it).
+      const float ph0 = start + rate * (float)l;
+      const float rev0 = __builtin_amdgcn_fractf(ph0 * INV_2PI);
+      const float revd = __builtin_amdgcn_fractf((rate * (float)T) * INV_2PI);
+      cf r{__builtin_amdgcn_cosf(rev0), __builtin_amdgcn_sinf(rev0)};
+      const cf wd{__builtin_amdgcn_cosf(revd), __builtin_amdgcn_sinf(revd)};
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        cf v = cmul_t<true>(in[q], r);
+        if (q + 1 < P) r = cmul_t<true>(r, wd);
+        if (hann) v = cscale(v, win[l + T * q]);
+        z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
+      }
+      return;
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < P; ++q) {
       const float ph = start + rate * (float)(l + T * q);
@@ -419,8 +445,9 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
 // FFT of the symbol held as pass-1 inputs in z (T lanes x P points) and the lane's
 // argmax key.  KEEP: leave the spectrum in natural order in `row` (padded address
 // paddr(bin)) for the estimate's neighbour bins; NPASS == 1 keeps it in z.
-template <int SF, bool KEEP, int ABL, bool FMA = false>
-__device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr) {
+template <int SF, bool KEEP, int ABL, bool FMA = false, bool TWL = false>
+__device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr,
+                                            const cf* twl = nullptr) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
   constexpr bool WL = G::WAVE_LOCAL;
@@ -454,10 +481,12 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
     constexpr int RL = G::NPASS == 2 ? G::RA : G::RB;   // last pass span
     constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
     constexpr int XA = ABL & 48;
+    // TWL: pass A's slot-major twiddles from the workgroup's LDS copy (k_demod_fast)
+    const cf* twA = TWL ? twl : a.twTA;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA, XA>(row, z, l, a.tw, key, a.twTA, second);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA, XA>(row, z, l, a.tw, key, twA, second);
     } else {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA, XA>(row, z, l, a.tw, key, a.twTA);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA, XA>(row, z, l, a.tw, key, twA);
       if (!(ABL & 16)) {
         block_sync<WL>();
         write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
@@ -595,6 +624,24 @@ constexpr int demod_waves_per_eu() {
   return SF >= 6 ? 4 : 1;
 }
 
+// Speculative demod: pass A's slot-major twiddles (15 or 3 per butterfly group, MA_A
+// groups: 48-240 values) are staged once per workgroup in LDS after the symbol rows, so
+// the pass reads them with ds_read instead of 15 vector loads per lane - the vector
+// memory path (texture addresser) is the demod's busiest unit.  Same values, same
+// arithmetic.  Returns the number of staged values (0: off).
+#ifndef LORA_TWA_LDS
+#define LORA_TWA_LDS 1
+#endif
+template <int SF, bool SPEC>
+constexpr int demod_twl_entries() {
+  if constexpr (!SPEC || !LORA_TWA_LDS || SF < 6) {
+    return 0;
+  } else {
+    using G = Geo<SF>;
+    return (G::RA == 16 ? 15 : 3) * G::MA_A;
+  }
+}
+
 // SPEC: the speculative single-read pipeline's symbol pass (lora_capi.hip): the pre-pass
 // offsets (fp_spec) on unscaled samples, and per data symbol (spec_marg, one 8-byte
 // store) the margin |X1| - |X2| between the top bin and the runner-up and the window's
@@ -639,8 +686,21 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   // dechirp product keeps the reference's arithmetic: the frame maximum (hence the scale,
   // cfo, time_offset and max_amp outputs) is taken over exactly these samples.
   constexpr bool FMA = SPEC && FAST;
+  constexpr int NTW = demod_twl_entries<SF, SPEC>();
+  static_assert(NTW <= 256, "one staged twiddle per thread");
+  cf* twl = rows + (size_t)SPW * rowc;
+  cf tv{0.0f, 0.0f};
+  if constexpr (NTW > 0) {  // issued first: it returns ahead of the symbol's gathers
+    if (tid < NTW) tv = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
+  }
   cf in[P], z[P];
   gather_points<SF, AB>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
+  if constexpr (NTW > 0) {
+    if (tid < NTW) twl[tid] = tv;
+    // wave-local kernels have no workgroup barrier before pass A; the others' first one
+    // (after the pass-1 write-back in fft_key) orders these writes
+    if constexpr (G::WAVE_LOCAL) __syncthreads();
+  }
   float pm = 0.0f;
   if constexpr (SPEC && !LORA_SPEC_ABL) {  // the window's dechirped, unscaled samples (scale is 1 here)
 #pragma unroll
@@ -649,8 +709,8 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   rotate_place<SF, !RAW, AB, FAST, FMA>(in, z, start, p.rate, hann, a.win, l);
   if constexpr (SPEC && !LORA_SPEC_ABL) asm volatile("" : "+v"(pm));
   float sec = 0.0f;
-  const uint64_t lkey =
-      fft_key<SF, false, AB, FMA>(z, rows + (size_t)g * rowc, l, a, SPEC && !LORA_SPEC_ABL ? &sec : nullptr);
+  const uint64_t lkey = fft_key<SF, false, AB, FMA, (NTW > 0)>(z, rows + (size_t)g * rowc, l, a,
+                                                               SPEC && !LORA_SPEC_ABL ? &sec : nullptr, twl);
   const uint64_t key = symbol_key<SF>(lkey, tid, red);
   if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + (s - s0)] = (uint16_t)key_index(key);
   if constexpr (SPEC && !LORA_SPEC_ABL) {
@@ -1041,7 +1101,14 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
           // complex products with fused multiply-adds: one rounding where the reference has
           // two, so E bounds its FFT and products as well.  Certified against the exact
           // reference like every other symbol.
-          const double fastd = (a.fast_rot || a.spec_hw) ? 4.0 * eps * rmax * L + 4e-7 : 0.0;
+          // With LORA_ROT_REC the demod takes one such factor r0 per lane (its first point)
+          // and one w for the step rate*T, then r_{q+1} = fma-product(r_q, w) for the lane's
+          // P = 16 points: |r_q - e^{i phi_q}| <= E_0 + q (e_w + 2 sqrt2 eps), with
+          // E_0 <= 2 eps |ph_0| + sqrt2 * 1.26e-7 and e_w <= 2 eps |rate T| + sqrt2 * 1.26e-7
+          // (|r|, |w| within 3e-6 of 1), so every factor is off by < 2 eps rmax L + 5.4e-6
+          // (|ph_0| + 15 |rate| T <= rmax L); doubled here.
+          const double hwd = LORA_ROT_REC ? 1.1e-5 : 4e-7;
+          const double fastd = (a.fast_rot || a.spec_hw) ? 4.0 * eps * rmax * L + hwd : 0.0;
           const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E + fastd);
           if (!(same_t && (double)d > 4.0 * B)) bad |= 1u << i;
         }
@@ -2082,7 +2149,7 @@ template <int SF, int MODE, int ABL = 0, bool FAST = false, bool SPEC = false>
 bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
-  const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * (size_t)G::SPW * rowc;
+  const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * ((size_t)G::SPW * rowc + demod_twl_entries<SF, SPEC>());
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
     if (hipFuncSetAttribute((const void*)k_demod_fast<SF, MODE, ABL, FAST, SPEC>,
