@@ -669,6 +669,7 @@ struct lora_demod_plan {
   uint16_t* rev;
   cf* twTA = nullptr;  // pass-A twiddles, slot-major (lora::twT_index), or null
   cf* twTB = nullptr;  // pass-B twiddles, slot-major, or null
+  cf* twTB2 = nullptr; // the same in slot pairs (16-byte loads), or null
   int use_fast;  // 0: generic LDS kernel only (LORA_MI355X_GENERIC=1, for A/B checks)
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), results invalid
   int max_chunks;  // 2-stream pipeline depth (LORA_MI355X_CHUNKS, default 1 = off)
@@ -785,7 +786,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   // group k]) so a wave instruction reads contiguous entries instead of a k-strided
   // gather.  Copies of the same table values: results unchanged (lora::twT_index).
   std::vector<std::complex<float>> twT;
-  int twTA_off = -1, twTB_off = -1;
+  int twTA_off = -1, twTB_off = -1, twTB2_off = -1;
   const char* twt_env = std::getenv("LORA_MI355X_TWT");  // A/B knob, read per plan
   const bool twt_ok = !(twt_env && twt_env[0] == '0');
   if (twt_ok && p.sf >= 6) {
@@ -799,6 +800,18 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
     };
     if (ps.RA > 1) twTA_off = add(ps.RA, ps.MA_A);
     if (ps.RB > 1) twTB_off = add(ps.RB, ps.MA_B);
+    if (ps.RB > 1) {  // pass B again in slot pairs (lora::KArgs::twTB2), 16-byte aligned
+      if (twT.size() & 1) twT.push_back(std::complex<float>(0.0f, 0.0f));
+      twTB2_off = (int)twT.size();
+      const int slots = ps.RB == 16 ? 15 : 3, MA = ps.MA_B;
+      for (int pp = 0; pp < slots / 2; ++pp)
+        for (int k = 0; k < MA; ++k) {
+          twT.push_back(tw[lora::twT_index(N, MA, 2 * pp, k)]);
+          twT.push_back(tw[lora::twT_index(N, MA, 2 * pp + 1, k)]);
+        }
+      if (slots & 1)
+        for (int k = 0; k < MA; ++k) twT.push_back(tw[lora::twT_index(N, MA, slots - 1, k)]);
+    }
   }
   const size_t b_tw = sizeof(cf) * N, b_down = sizeof(cf) * 2 * step, b_down1 = sizeof(cf) * N,
                b_win = sizeof(float) * N, b_rev = sizeof(uint16_t) * N, b_twT = sizeof(cf) * twT.size();
@@ -855,6 +868,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   cf* twT_dev = twT.empty() ? nullptr : reinterpret_cast<cf*>(b);
   plan->twTA = twTA_off >= 0 ? twT_dev + twTA_off : nullptr;
   plan->twTB = twTB_off >= 0 ? twT_dev + twTB_off : nullptr;
+  plan->twTB2 = twTB2_off >= 0 ? twT_dev + twTB2_off : nullptr;
   b += al(b_twT);
   plan->spec_fix = reinterpret_cast<unsigned int*>(b);
   hipError_t e = hipStreamCreateWithFlags(&plan->aux, hipStreamNonBlocking);
@@ -1001,6 +1015,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.down1 = plan->down1;
   a.twTA = plan->twTA;
   a.twTB = plan->twTB;
+  a.twTB2 = plan->twTB2;
   unsigned char* wsb = static_cast<unsigned char*>(workspace);
   uint32_t* maxbits = reinterpret_cast<uint32_t*>(wsb);
   a.maxbits = maxbits;

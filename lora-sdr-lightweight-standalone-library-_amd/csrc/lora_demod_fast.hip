@@ -205,6 +205,29 @@ __device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__
   }
 }
 
+// pass_regs_T with the twiddles in slot pairs (KArgs::twTB2): one 16-byte load per two.
+template <int R, int MA, bool FMA = false>
+__device__ __forceinline__ void pass_regs_T2(cf* x, int k, const cf* __restrict__ twT2) {
+  static_assert(R == 4 || R == 16, "radix-4 / radix-16 passes");
+  constexpr int NT = R == 16 ? 15 : 3;
+  cf w[NT];
+  const float4* __restrict__ p4 = reinterpret_cast<const float4*>(twT2);
+#pragma unroll
+  for (int pp = 0; pp < NT / 2; ++pp) {
+    const float4 v = p4[pp * MA + k];
+    w[2 * pp] = cf{v.x, v.y};
+    w[2 * pp + 1] = cf{v.z, v.w};
+  }
+  w[NT - 1] = twT2[(NT / 2) * MA * 2 + k];
+#pragma unroll
+  for (int blk = 0; blk < R; blk += 4) bfly4<FMA>(x[blk], x[blk + 1], x[blk + 2], x[blk + 3], w[0], w[1], w[2]);
+  if constexpr (R == 16) {
+#pragma unroll
+    for (int uu = 0; uu < 4; ++uu)
+      bfly4<FMA>(x[uu], x[uu + 4], x[uu + 8], x[uu + 12], w[3 + 3 * uu], w[4 + 3 * uu], w[5 + 3 * uu]);
+  }
+}
+
 // The other lanes' share of one pass: read R points from LDS, run the stages,
 // either write them back or fold them into the argmax key.
 #ifndef LORA_SPEC_ABL
@@ -217,7 +240,7 @@ __device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__
 // XA: profiling-only ablation bits of the speculative kernel (LORA_SPEC_ABLX, results
 // invalid): 16 = no LDS reads (the lane's own values stand in), 32 = one twiddle load
 // per group instead of one per butterfly input.
-template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false, int XA = 0>
+template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false, int XA = 0, bool PAIR = false>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
                                          uint64_t& key, const cf* __restrict__ twT = nullptr,
                                          float* second = nullptr) {
@@ -244,7 +267,10 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     }
     if constexpr (R == 4 || R == 16) {
       if (twT) {
-        pass_regs_T<R, MA, FMA>(xs, k, twT);
+        if constexpr (PAIR)
+          pass_regs_T2<R, MA, FMA>(xs, k, twT);
+        else
+          pass_regs_T<R, MA, FMA>(xs, k, twT);
         continue;
       }
     }
@@ -355,6 +381,14 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 
 // CFO rotation (glibc-faithful sincosf, LoRaDemod.cpp:151-157) when ROT, window
 // (:158-160), and placement in pass-1 leaf order.
+// Speculative demod table access (A/B knobs): pass-A twiddles staged in LDS, pass-B
+// twiddles in slot pairs (KArgs::twTB2).
+#ifndef LORA_TWA_LDS
+#define LORA_TWA_LDS 1
+#endif
+#ifndef LORA_TWB_PAIR
+#define LORA_TWB_PAIR 1  // ... and pass B's twiddles in slot pairs (KArgs::twTB2)
+#endif
 #ifndef LORA_ROT_REC
 #define LORA_ROT_REC 1  // certified demod: rotation factors by recurrence (0: one sin/cos pair per point)
 #endif
@@ -492,7 +526,9 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
         write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
         block_sync<WL>();
       }
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, XA>(row, z, l, a.tw, key, a.twTB, second);
+      // TWL (speculative demod): pass B's twiddles two per 16-byte load (KArgs::twTB2)
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, XA, TWL && LORA_TWB_PAIR>(
+          row, z, l, a.tw, key, (TWL && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)
@@ -629,9 +665,6 @@ constexpr int demod_waves_per_eu() {
 // the pass reads them with ds_read instead of 15 vector loads per lane - the vector
 // memory path (texture addresser) is the demod's busiest unit.  Same values, same
 // arithmetic.  Returns the number of staged values (0: off).
-#ifndef LORA_TWA_LDS
-#define LORA_TWA_LDS 1
-#endif
 template <int SF, bool SPEC>
 constexpr int demod_twl_entries() {
   if constexpr (!SPEC || !LORA_TWA_LDS || SF < 6) {

@@ -34,6 +34,9 @@ struct KArgs {
   int fast_rot;  // LORA_PRECISION_FAST: hardware sin/cos rotation in the symbol demod
   const cf* twTA;  // fast kernels: slot-major twiddles of LDS pass A / B (or null)
   const cf* twTB;
+  // twTB in slot pairs: float4 {slot 2p, slot 2p+1} at [p*MA + k], an odd last slot after
+  // them as cf at [(NT/2)*MA*2 + k] - one 16-byte load per two twiddles (or null)
+  const cf* twTB2;
   // Speculative single-read pipeline (lora_demod_batch, LEGACY osr-1 unwindowed frames):
   // the estimate on unscaled samples, the data symbols' window maxima and certification
   // margins written by the symbol demod, and a device counter of exact recomputations.
