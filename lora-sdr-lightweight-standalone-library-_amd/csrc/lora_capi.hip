@@ -670,6 +670,7 @@ struct lora_demod_plan {
   cf* twTA = nullptr;  // pass-A twiddles, slot-major (lora::twT_index), or null
   cf* twTB = nullptr;  // pass-B twiddles, slot-major, or null
   cf* twTB2 = nullptr; // the same in slot pairs (16-byte loads), or null
+  cf* downP = nullptr;  // dechirp-table pairs of the speculative demod (osr 1), or null
   int use_fast;  // 0: generic LDS kernel only (LORA_MI355X_GENERIC=1, for A/B checks)
   int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), results invalid
   int max_chunks;  // 2-stream pipeline depth (LORA_MI355X_CHUNKS, default 1 = off)
@@ -813,6 +814,21 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
         for (int k = 0; k < MA; ++k) twT.push_back(tw[lora::twT_index(N, MA, slots - 1, k)]);
     }
   }
+  // The speculative demod's dechirp-table pairs (lora::KArgs::downP, osr 1): lane l of a
+  // window at table phase cg multiplies its points q = 2p, 2p+1 by down[cg + l + T*q];
+  // stored as one 16-byte entry per (p, c = cg + l), c < N + T, so a wave instruction reads
+  // 64 consecutive entries.  Copies of the same values (the doubled table needs no wrap).
+  int downP_off = -1;
+  if (twt_ok && p.sf >= 6 && p.osr == 1) {
+    if (twT.size() & 1) twT.push_back(std::complex<float>(0.0f, 0.0f));
+    downP_off = (int)twT.size();
+    const int T = N / 16, C = N + T;
+    for (int pp = 0; pp < 8; ++pp)
+      for (int c = 0; c < C; ++c) {
+        twT.push_back(down[c + T * 2 * pp]);
+        twT.push_back(down[c + T * (2 * pp + 1)]);
+      }
+  }
   const size_t b_tw = sizeof(cf) * N, b_down = sizeof(cf) * 2 * step, b_down1 = sizeof(cf) * N,
                b_win = sizeof(float) * N, b_rev = sizeof(uint16_t) * N, b_twT = sizeof(cf) * twT.size();
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -869,6 +885,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   plan->twTA = twTA_off >= 0 ? twT_dev + twTA_off : nullptr;
   plan->twTB = twTB_off >= 0 ? twT_dev + twTB_off : nullptr;
   plan->twTB2 = twTB2_off >= 0 ? twT_dev + twTB2_off : nullptr;
+  plan->downP = downP_off >= 0 ? twT_dev + downP_off : nullptr;
   b += al(b_twT);
   plan->spec_fix = reinterpret_cast<unsigned int*>(b);
   hipError_t e = hipStreamCreateWithFlags(&plan->aux, hipStreamNonBlocking);
@@ -1016,6 +1033,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.twTA = plan->twTA;
   a.twTB = plan->twTB;
   a.twTB2 = plan->twTB2;
+  a.downP = plan->downP;
   unsigned char* wsb = static_cast<unsigned char*>(workspace);
   uint32_t* maxbits = reinterpret_cast<uint32_t*>(wsb);
   a.maxbits = maxbits;

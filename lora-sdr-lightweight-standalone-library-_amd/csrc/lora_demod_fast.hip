@@ -341,12 +341,27 @@ __device__ __forceinline__ void sym_base(int s, int step, int64_t frame_len, int
 // and apply what precedes the rotation: KIND 0 raw (API estimate, phy.cpp:91-99),
 // KIND 1 LEGACY (caller dechirp, e2e_chain_test.cpp:88-93, then normalisation,
 // LoRaDemod.cpp:68-77), KIND 2 API down-chirp (phy.cpp:216-225).
-template <int SF, int ABL>
+template <int SF, int ABL, bool PAIRD = false>
 __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restrict__ x, int l,
                                               int osr, int step, int cg, int kind, bool dech,
                                               float scale, cf* in) {
   using G = Geo<SF>;
   constexpr int T = G::T, P = G::P;
+  if constexpr (PAIRD && P == 16 && !(ABL & 12)) {
+    // speculative demod, LEGACY osr 1 with the fused dechirp: the table values two per
+    // 16-byte load from KArgs::downP (same values, same products)
+    const cf* __restrict__ xl = x + l;
+#pragma unroll
+    for (int q = 0; q < P; ++q) in[q] = xl[T * q];
+    const float4* __restrict__ dp = reinterpret_cast<const float4*>(a.downP) + cg + l;
+#pragma unroll
+    for (int pp = 0; pp < P / 2; ++pp) {
+      const float4 d = dp[pp * (G::N + T)];
+      in[2 * pp] = cmul(in[2 * pp], cf{d.x, d.y});
+      in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{d.z, d.w});
+    }
+    return;
+  }
   // One per-lane base pointer per stream; the points are then at compile-time offsets
   // T*q (times osr) from it, which fold into the loads' immediate offsets at osr 1.
   const cf* __restrict__ xl = x + (int64_t)l * osr;
@@ -385,6 +400,9 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 // twiddles in slot pairs (KArgs::twTB2).
 #ifndef LORA_TWA_LDS
 #define LORA_TWA_LDS 1
+#endif
+#ifndef LORA_DECH_PAIR
+#define LORA_DECH_PAIR 1  // ... and the fused dechirp's table values in pairs (KArgs::downP)
 #endif
 #ifndef LORA_TWB_PAIR
 #define LORA_TWB_PAIR 1  // ... and pass B's twiddles in slot pairs (KArgs::twTB2)
@@ -727,7 +745,10 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
     if (tid < NTW) tv = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
   }
   cf in[P], z[P];
-  gather_points<SF, AB>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
+  if (SPEC && LORA_DECH_PAIR && MODE == 0 && a.downP)  // the speculative demod's scale is 1
+    gather_points<SF, AB, true>(a, x, l, 1, N, cg, 1, true, 1.0f, in);
+  else
+    gather_points<SF, AB>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
   if constexpr (NTW > 0) {
     if (tid < NTW) twl[tid] = tv;
     // wave-local kernels have no workgroup barrier before pass A; the others' first one

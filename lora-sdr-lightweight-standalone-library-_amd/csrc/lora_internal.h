@@ -37,6 +37,9 @@ struct KArgs {
   // twTB in slot pairs: float4 {slot 2p, slot 2p+1} at [p*MA + k], an odd last slot after
   // them as cf at [(NT/2)*MA*2 + k] - one 16-byte load per two twiddles (or null)
   const cf* twTB2;
+  // LEGACY osr-1 dechirp table in pairs (speculative demod): float4 {down[c + T*2p],
+  // down[c + T*(2p+1)]} at [p*(N + T) + c], T = N/16, c < N + T (or null)
+  const cf* downP;
   // Speculative single-read pipeline (lora_demod_batch, LEGACY osr-1 unwindowed frames):
   // the estimate on unscaled samples, the data symbols' window maxima and certification
   // margins written by the symbol demod, and a device counter of exact recomputations.
