@@ -309,3 +309,44 @@ def test_max_amp_is_the_reference_frame_maximum(O, amd, sf, dechirp, path):
         np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
         assert bits(res.cfo[f].item()) == bits(ocfo)
         assert bits(res.time_offset[f].item()) == bits(otoff)
+
+
+@pytest.mark.parametrize("sf,S,F", [(7, 81, 24), (9, 81, 8), (12, 24, 4)])
+@pytest.mark.parametrize("snr_db", [10, -5])
+def test_fused_dechirp_large_cfo_and_delay(O, amd, sf, S, F, snr_db):
+    """The benchmark's path (LEGACY, fused caller dechirp): frames with a carrier offset of
+    up to +-0.45 bin, a random sample delay (so t_off != 0 and every window starts at a
+    table phase cg != 0 of the paired dechirp table) and the longest eligible frames (81
+    symbols: the largest rotation phases the certification bound must cover, which for the
+    recurrence-built rotation factors grows with rate * L), against the oracle on the
+    caller-dechirped frames, bit for bit."""
+    N = 1 << sf
+    rng = np.random.default_rng(7000 + 10 * sf + snr_db)
+    L = S * N
+    iq = np.zeros((F, L), np.complex64)
+    for f in range(F):
+        syms = rng.integers(0, N, S - 2).astype(np.uint16)
+        x = O.lora_modulate(syms, sf, 1, 125000, 1.0, int(rng.integers(0, 256))).astype(np.complex128)
+        cfo = rng.uniform(-0.45, 0.45)
+        x = x * np.exp(2j * np.pi * cfo * np.arange(len(x)) / N)
+        d = int(rng.integers(1, N // 3))
+        x = np.concatenate([np.zeros(d), x])[:L]
+        amp = rng.uniform(0.7, 1.5)
+        sigma = amp * 10 ** (-snr_db / 20) / np.sqrt(2)
+        x = amp * x + sigma * (rng.standard_normal(L) + 1j * rng.standard_normal(L))
+        iq[f] = x.astype(np.complex64)
+    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True)
+    res = plan.run(torch.from_numpy(iq).cuda())
+    torch.cuda.synchronize()
+    assert "spec" in plan.last_kernels()
+    syms = res.symbols.cpu().numpy()
+    nz = 0
+    for f in range(F):
+        xd = O.dechirp(iq[f], sf, 1)
+        osym, osync, ocfo, otoff = O.lora_demodulate(xd, sf, 1, False)
+        np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
+        assert int(res.sync[f]) == osync
+        assert bits(res.cfo[f].item()) == bits(ocfo)
+        assert bits(res.time_offset[f].item()) == bits(otoff)
+        nz += otoff != 0
+    assert nz > 0, "no frame exercised a non-zero time offset"
