@@ -4,7 +4,9 @@ One step = one lora_demod_batch over this rank's batch of frames already residen
 HBM: LEGACY lora_demodulate semantics with the fused caller-side dechirp
 (e2e_chain_test.cpp:85-101): normalisation, 2-symbol CFO/timing estimate, per-symbol
 CFO rotation, FFT, argmax, sync word.  Inputs are generated on the device by the
-bit-exact GPU modulator (lora_mod_batch), random symbols from a fixed seed.
+bit-exact GPU modulator (lora_mod_batch), random symbols from a fixed seed.  The step's
+launches are captured once into a HIP graph and replayed per step (`--launch eager`:
+plan.run per step, ~1.5 % slower at SF7 from host launch overhead).
 
 Headline workload (BASELINE.json configs[1]): SF7 BW125 osr 1, 1,000,000 data symbols
 = 15,625 frames x (2 sync + 64 data) per GPU.  The SF12 configuration (configs[2]) and
@@ -151,6 +153,9 @@ def make_input(sf, frames, data_syms, seed, device, snr_db=None, sync=None):
     return syms, iq
 
 
+LAUNCH = "graph"  # --launch: "graph" (HIP graph replay of the step, default) or "eager" (plan.run)
+
+
 def stage_times(plan, iq, out, steps, device):
     """Per-kernel durations: a second pass of the same steps with HIP events around every
     launch, recorded on the stream each kernel runs on (outside the timed region)."""
@@ -187,12 +192,30 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     for _ in range(warmup):
         out = plan.run(iq, out)
     torch.cuda.synchronize(device)
+    step = None
+    if LAUNCH == "graph":
+        # the step's launches captured once into a HIP graph and replayed (the same kernels
+        # on the same buffers; lora_demod_batch enqueues only kernels, no sync or allocation)
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            out = plan.run(iq, out)
+        torch.cuda.current_stream(device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = plan.run(iq, out)
+        step = g.replay
+        step()
+        torch.cuda.synchronize(device)
     fixed0 = plan.spec_recomputed()
     barrier(dist)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(steps):
-        out = plan.run(iq, out)
+        if step is not None:
+            step()
+        else:
+            out = plan.run(iq, out)
     torch.cuda.synchronize(device)
     barrier(dist)
     wall = time.perf_counter() - t0
@@ -453,6 +476,9 @@ def roofline(r, probe=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--launch", choices=["eager", "graph"], default="graph",
+                    help="step launch: one HIP-graph replay of the step's launches (default; the same "
+                         "kernels on the same buffers, captured once), or plan.run per step")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=15625)
@@ -471,6 +497,8 @@ def main():
                     help="form the ranks and report them without touching a GPU (CPU test of the "
                          "multi-rank launch)")
     args = ap.parse_args()
+    global LAUNCH
+    LAUNCH = args.launch
     global SYNC
     SYNC = args.sync
 
@@ -569,7 +597,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (GPU lora_modulate of seeded random symbols, amplitude 1, no noise)",
-            "config": {"workload": workload, "sf": 7, "bw_hz": 125000, "osr": 1,
+            "config": {"workload": workload, "launch": LAUNCH, "sf": 7, "bw_hz": 125000, "osr": 1,
                        "frames_per_gpu": args.frames, "data_symbols_per_frame": args.data_symbols,
                        "parallelism": f"frames sharded x{world}, no collective (gloo timing only)",
                        "ranks": ranks, "symbols_ok": r7["symbols_ok"], "stage_ms": r7["stage_ms"],
