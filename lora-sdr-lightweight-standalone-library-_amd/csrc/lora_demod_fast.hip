@@ -351,8 +351,19 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
     // speculative demod, LEGACY osr 1 with the fused dechirp: the table values two per
     // 16-byte load from KArgs::downP (same values, same products)
     const cf* __restrict__ xl = x + l;
+#if LORA_IQ_NT
+    // each sample is read once: nontemporal loads leave the caches to the tables
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    const v2f* __restrict__ xl2 = reinterpret_cast<const v2f*>(xl);
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const v2f v = __builtin_nontemporal_load(xl2 + T * q);
+      in[q] = cf{v.x, v.y};
+    }
+#else
 #pragma unroll
     for (int q = 0; q < P; ++q) in[q] = xl[T * q];
+#endif
     const float4* __restrict__ dp = reinterpret_cast<const float4*>(a.downP) + cg + l;
 #pragma unroll
     for (int pp = 0; pp < P / 2; ++pp) {
@@ -403,6 +414,9 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 #endif
 #ifndef LORA_DECH_PAIR
 #define LORA_DECH_PAIR 1  // ... and the fused dechirp's table values in pairs (KArgs::downP)
+#endif
+#ifndef LORA_IQ_NT
+#define LORA_IQ_NT 1  // nontemporal sample loads in the paired-table gather (step -0.6 to -0.8 %)
 #endif
 #ifndef LORA_TWB_PAIR
 #define LORA_TWB_PAIR 1  // ... and pass B's twiddles in slot pairs (KArgs::twTB2)
