@@ -418,6 +418,9 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 #ifndef LORA_IQ_NT
 #define LORA_IQ_NT 1  // nontemporal sample loads in the paired-table gather (step -0.6 to -0.8 %)
 #endif
+#ifndef LORA_EST_TWB_PAIR
+#define LORA_EST_TWB_PAIR 1  // ... also in every other transform (estimate, recompute)
+#endif
 #ifndef LORA_TWB_PAIR
 #define LORA_TWB_PAIR 1  // ... and pass B's twiddles in slot pairs (KArgs::twTB2)
 #endif
@@ -559,8 +562,8 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
         block_sync<WL>();
       }
       // TWL (speculative demod): pass B's twiddles two per 16-byte load (KArgs::twTB2)
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, XA, TWL && LORA_TWB_PAIR>(
-          row, z, l, a.tw, key, (TWL && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, XA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR>(
+          row, z, l, a.tw, key, ((TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)
