@@ -479,8 +479,10 @@ def main():
     ap.add_argument("--launch", choices=["eager", "graph"], default="graph",
                     help="step launch: one HIP-graph replay of the step's launches (default; the same "
                          "kernels on the same buffers, captured once), or plan.run per step")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 100 timed steps (33 ms at SF7): with 20 (6 ms) a single host or clock hiccup moved the
+    # per-step time by several percent between runs of the same build
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--frames", type=int, default=15625)
     ap.add_argument("--data-symbols", type=int, default=64)
     ap.add_argument("--sf12-frames", type=int, default=15625)
