@@ -26,8 +26,7 @@
  * device memory (HBM) of the plan's device.  The caller owns every buffer
  * (API_SPEC.md ownership rule); the plan owns only its constant tables.  No call
  * allocates or synchronises: `stream` is a hipStream_t (NULL = default stream); the
- * work is enqueued on it (lora_demod_batch forks large batches onto the plan's
- * auxiliary stream and joins back with events), so the calls are hipGraph-capturable.
+ * work is enqueued on it and nothing else, so the calls are hipGraph-capturable.
  * A plan may be used by one host thread at a time.
  *
  * Errors are negative errno values (the reference returns -1, phy.cpp:27,58,181-190);
@@ -156,25 +155,23 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
 
 /* Measurement hooks (bench.py): while enabled, every kernel lora_demod_batch launches
  * on this plan is bracketed by a pair of HIP events on the stream it runs on, for up
- * to `max_calls` calls.  Stages: 0 = frame max, 1 = estimate + sync symbols,
- * 2 = symbol demod.  lora_demod_profile_read waits for the recorded events and
- * returns, per stage, the summed kernel ms over the recorded calls (stage_ms[3]) and
- * the number of calls recorded.  Large batches are pipelined in chunks (prep of
- * chunk c+1 on the plan's auxiliary stream overlaps demod of chunk c on `stream`),
- * so stage times can overlap and need not add up to the wall time.  No effect on
- * results. */
+ * to `max_calls` calls.  Stages: 0 = frame max, 1 = estimate + sync symbols (with the
+ * speculative pipeline: its pre-pass and certification kernels), 2 = symbol demod.
+ * lora_demod_profile_read waits for the recorded events and returns, per stage, the
+ * summed kernel ms over the recorded calls (stage_ms[3]) and the number of calls
+ * recorded.  No effect on results. */
 int lora_demod_profile_enable(lora_demod_plan* plan, int max_calls);
 int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls);
 
 /* Which kernels the plan's last lora_demod_batch call launched (bit mask, for tests and
- * measurement): the three-launch path is FRAME_MAX (LEGACY) + ESTIMATE + DEMOD; the
- * frame-resident single-read kernel (LEGACY, osr 1, no window, SF 6-8, frames whose LDS
- * image fits) is FUSED alone; GENERIC marks the LDS reference kernels.  0 before the
- * first call.  Host-side bookkeeping only. */
+ * measurement): the speculative single-read pipeline is SPEC + ESTIMATE + DEMOD; the
+ * three-launch path is FRAME_MAX (LEGACY) + ESTIMATE + DEMOD; GENERIC marks the LDS
+ * estimate kernel (frames with fewer than two whole symbols).  0 before the first call.
+ * Host-side bookkeeping only.  (Bit 8 belonged to a frame-resident kernel that measured
+ * slower and was removed; it is never set.) */
 #define LORA_KERNEL_FRAME_MAX 1
 #define LORA_KERNEL_ESTIMATE 2
 #define LORA_KERNEL_DEMOD 4
-#define LORA_KERNEL_FUSED 8
 #define LORA_KERNEL_GENERIC 16
 #define LORA_KERNEL_FRAME_MAX_WAVE 32 /* with FRAME_MAX: the one-wave-per-frame variant (short frames) */
 #define LORA_KERNEL_SPEC 64 /* the speculative single-read pipeline (with ESTIMATE + DEMOD) */

@@ -473,59 +473,6 @@ __global__ void __launch_bounds__(256) k_frame_max_wave(KArgs a, int64_t frames,
   if (t == 0) maxbits[f] = __float_as_uint(m);
 }
 
-// G symbols per workgroup; work item w -> (frame, symbol) over the symbols that are
-// not sync symbols.
-__global__ void __launch_bounds__(256) k_demod(KArgs a, int G, int s0, int64_t work) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  cf* A = reinterpret_cast<cf*>(smem);
-  const int N = a.N;
-  const int per = a.total - s0;
-  const int64_t w0 = (int64_t)blockIdx.x * G;
-  const int P = G * N;
-  for (int q = threadIdx.x; q < P; q += blockDim.x) {
-    const int g = q >> a.sf;
-    const int i = q & (N - 1);
-    const int64_t w = w0 + g;
-    cf v = {0.0f, 0.0f};
-    if (w < work) {
-      const int64_t f = w / per;
-      const int s = s0 + (int)(w - f * per);
-      const lora::FrameParams p =
-          a.mode == LORA_MODE_RAW ? lora::FrameParams{0.0f, 0.0f, 0.0f, 1.0f, 0, 0, 0, 0} : a.fp[f];
-      v = symbol_point(a, a.iq + f * a.frame_stride, p, s, i);
-    }
-    A[g * N + a.rev[i]] = v;
-  }
-  __syncthreads();
-  lora::fft_lds(A, a.sf, G, a.tw, threadIdx.x, blockDim.x);
-  // Argmax: T = 256/G threads per symbol.
-  const int T = blockDim.x / G;
-  const int g = threadIdx.x / T;
-  const int lt = threadIdx.x % T;
-  uint64_t k = 0;
-  for (int i = lt; i < N; i += T) k = lora::umax64(k, lora::argmax_key(A[g * N + i], i));
-  __shared__ uint64_t red[4];
-  if (T <= 64) {
-    k = lora::group_max(k, T);
-  } else {
-    k = lora::group_max(k, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = k;
-    __syncthreads();
-    const int wpg = T >> 6;
-    const int wb = (threadIdx.x >> 6) / wpg * wpg;
-    k = red[wb];
-    for (int u = 1; u < wpg; ++u) k = lora::umax64(k, red[wb + u]);
-  }
-  if (lt == 0) {
-    const int64_t w = w0 + g;
-    if (w < work && a.syms) {
-      const int64_t f = w / per;
-      const int s = (int)(w - f * per);
-      a.syms[f * a.sym_stride + s] = (uint16_t)lora::key_index(k);
-    }
-  }
-}
-
 // phy.cpp:147-176 (compensate_offsets), out of place: rotation by rate*n first,
 // then the integer shift with zero fill.
 __global__ void __launch_bounds__(256) k_compensate(const cf* __restrict__ in, cf* __restrict__ out,
@@ -671,19 +618,9 @@ struct lora_demod_plan {
   cf* twTB = nullptr;  // pass-B twiddles, slot-major, or null
   cf* twTB2 = nullptr; // the same in slot pairs (16-byte loads), or null
   cf* downP = nullptr;  // dechirp-table pairs of the speculative demod (osr 1), or null
-  int use_fast;  // 0: generic LDS kernel only (LORA_MI355X_GENERIC=1, for A/B checks)
-  int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), results invalid
-  int max_chunks;  // 2-stream pipeline depth (LORA_MI355X_CHUNKS, default 1 = off)
-  size_t fused_lds_max;  // frame-resident single-read kernel: LDS image limit (0 = off)
   int spec;              // speculative single-read pipeline enabled (LORA_MI355X_SPEC, default 1)
-  int spec_hw;           // ... with the hardware-sin/cos rotation + certification (LORA_MI355X_SPEC_HW, default 1)
   unsigned int* spec_fix = nullptr;  // device counter of symbols the pipeline recomputed
   int last_kernels = 0;  // LORA_KERNEL_* mask of the last lora_demod_batch call
-  // Two-stream pipeline: per-frame prep (max + estimate) of chunk c+1 on `aux`
-  // overlaps the symbol demod of chunk c on the caller's stream.
-  hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr;
-  hipEvent_t ev_chunk[16] = {};
   // measurement hooks (lora_demod_profile_enable): per kernel launch (stage, begin, end)
   struct ProfRec {
     int stage;
@@ -695,7 +632,6 @@ struct lora_demod_plan {
 };
 
 namespace {
-constexpr int kMaxChunks = 16;
 
 // Event pair around one kernel launch (profiling only; no-op when disabled).
 struct ProfScope {
@@ -788,9 +724,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   // gather.  Copies of the same table values: results unchanged (lora::twT_index).
   std::vector<std::complex<float>> twT;
   int twTA_off = -1, twTB_off = -1, twTB2_off = -1;
-  const char* twt_env = std::getenv("LORA_MI355X_TWT");  // A/B knob, read per plan
-  const bool twt_ok = !(twt_env && twt_env[0] == '0');
-  if (twt_ok && p.sf >= 6) {
+  if (p.sf >= 6) {
     lora::PassShape ps = lora::pass_shape((int)p.sf);
     auto add = [&](int R, int MA) {
       const int off = (int)twT.size();
@@ -819,7 +753,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   // stored as one 16-byte entry per (p, c = cg + l), c < N + T, so a wave instruction reads
   // 64 consecutive entries.  Copies of the same values (the doubled table needs no wrap).
   int downP_off = -1;
-  if (twt_ok && p.sf >= 6 && p.osr == 1) {
+  if (p.sf >= 6 && p.osr == 1) {
     if (twT.size() & 1) twT.push_back(std::complex<float>(0.0f, 0.0f));
     downP_off = (int)twT.size();
     const int T = N / 16, C = N + T;
@@ -849,26 +783,10 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   plan->step = step;
   plan->power_scale = 20 * std::log10(static_cast<size_t>(N));  // LoRaDetector.hpp:29
   {
-    const char* g = std::getenv("LORA_MI355X_GENERIC");
-    plan->use_fast = (g && g[0] == '1') ? 0 : 1;
-    const char* ab = std::getenv("LORA_MI355X_ABLATE");
-    plan->ablate = ab ? std::atoi(ab) : 0;
-    if (plan->ablate)
-      std::fprintf(stderr, "lora_mi355x: LORA_MI355X_ABLATE=%d - profiling ablation, demodulation results are "
-                           "INVALID for this plan\n", plan->ablate);
-    const char* ch = std::getenv("LORA_MI355X_CHUNKS");
-    plan->max_chunks = std::max(1, std::min(kMaxChunks, ch ? std::atoi(ch) : 1));
-    // Frame-resident single-read kernel (k_frame_fused), opt-in: LORA_MI355X_FUSED = its LDS
-    // image limit in KiB (80 = two frames per CU), unset or 0 = off.  It is bit-exact but
-    // slower than the three launches on the measured workloads:
-    // its per-frame estimate chain is serial latency that two frames per CU cannot hide.
+    // The one diagnostic knob: LORA_MI355X_SPEC=0 runs the three-launch path (frame max,
+    // estimate, demod) instead of the speculative single-read pipeline.
     const char* sp = std::getenv("LORA_MI355X_SPEC");
     plan->spec = !(sp && sp[0] == '0');
-    const char* sh = std::getenv("LORA_MI355X_SPEC_HW");
-    plan->spec_hw = !(sh && sh[0] == '0');
-    const char* fu = std::getenv("LORA_MI355X_FUSED");
-    const int fk = fu ? std::max(0, std::min(160, std::atoi(fu))) : 0;
-    plan->fused_lds_max = fk == 0 ? 0 : (size_t)fk * 1024 - (fk <= 80 ? 256 : 128);
   }
   plan->dev_tables = mem;
   plan->tw = reinterpret_cast<cf*>(b);
@@ -888,11 +806,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   plan->downP = downP_off >= 0 ? twT_dev + downP_off : nullptr;
   b += al(b_twT);
   plan->spec_fix = reinterpret_cast<unsigned int*>(b);
-  hipError_t e = hipStreamCreateWithFlags(&plan->aux, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->ev_fork, hipEventDisableTiming);
-  for (int c = 0; c < kMaxChunks && e == hipSuccess; ++c)
-    e = hipEventCreateWithFlags(&plan->ev_chunk[c], hipEventDisableTiming);
-  if (e == hipSuccess) e = hipMemcpy(plan->tw, tw.data(), b_tw, hipMemcpyHostToDevice);
+  hipError_t e = hipMemcpy(plan->tw, tw.data(), b_tw, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->down, down.data(), b_down, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->down1, down1.data(), b_down1, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(plan->win, win.data(), b_win, hipMemcpyHostToDevice);
@@ -902,7 +816,7 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   hipSetDevice(prev);
   if (e != hipSuccess) {
     const std::string msg = std::string("plan setup: ") + hipGetErrorString(e);
-    lora_demod_plan_destroy(plan);  // streams / events created so far, and the tables
+    lora_demod_plan_destroy(plan);  // the tables
     return set_error(LORA_EIO, msg);
   }
   *out = plan;
@@ -920,7 +834,7 @@ int lora_demod_profile_enable(lora_demod_plan* plan, int max_calls) {
   }
   for (hipEvent_t e : plan->prof_pool) hipEventDestroy(e);
   plan->prof_recs.clear();
-  plan->prof_pool.assign((size_t)max_calls * 3 * kMaxChunks * 2, nullptr);
+  plan->prof_pool.assign((size_t)max_calls * 3 * 2, nullptr);
   for (auto& e : plan->prof_pool) HIP_TRY(hipEventCreate(&e));
   plan->prof_max = max_calls;
   plan->prof_calls = 0;
@@ -951,10 +865,6 @@ int lora_demod_plan_destroy(lora_demod_plan* plan) {
     hipEventDestroy(r.e);
   }
   for (hipEvent_t e : plan->prof_pool) hipEventDestroy(e);
-  if (plan->aux) hipStreamDestroy(plan->aux);
-  if (plan->ev_fork) hipEventDestroy(plan->ev_fork);
-  for (hipEvent_t e : plan->ev_chunk)
-    if (e) hipEventDestroy(e);
   hipFree(plan->dev_tables);
   hipSetDevice(prev);
   delete plan;
@@ -1049,28 +959,18 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.toff = out->time_offset;
   a.max_amp = out->max_amp;
   a.est_only = 0;
-  a.ablate = plan->ablate;
   a.fast_rot = (p.precision == LORA_PRECISION_FAST && p.mode != LORA_MODE_RAW) ? 1 : 0;
 
   const int s0 = a.have_sync ? 2 : 0;
   const int64_t per = total - s0;
-  // samples per k_frame_max block (experiment knob LORA_MI355X_MAXCHUNK, default 4096)
-  static const int max_chunk = [] {
-    const char* e = std::getenv("LORA_MI355X_MAXCHUNK");
-    const int v = e ? std::atoi(e) : 4096;
-    return v >= 512 ? v : 4096;
-  }();
-  // Blocks per frame rounded DOWN, so each block streams at least one full batch
-  // (256 threads x 8 pairs = 4096 samples): SF7 frames of 8448 samples as 2 x 4224
-  // (0.17 ms) rather than 3 x 2816 (0.185 ms, partly idle batches); SF12 66 x 4096.
-  const int bpf = frame_len > 0 ? (int)std::min<int64_t>(lora::kMaxBpf, std::max<int64_t>(1, frame_len / max_chunk))
+  // k_frame_max: blocks per frame rounded DOWN, so each block streams at least one full
+  // batch of 4096 samples (256 threads x 8 pairs): SF7 frames of 8448 samples as 2 x 4224
+  // rather than 3 x 2816 (partly idle batches); SF12 66 x 4096.  Frames shorter than two
+  // batches take one wave each (k_frame_max_wave).
+  constexpr int kMaxChunk = 4096;
+  const int bpf = frame_len > 0 ? (int)std::min<int64_t>(lora::kMaxBpf, std::max<int64_t>(1, frame_len / kMaxChunk))
                                 : 1;
-  // frames shorter than two batches: one wave per frame (k_frame_max_wave)
-  static const bool wave_ok = [] {
-    const char* e = std::getenv("LORA_MI355X_MAXWAVE");
-    return !(e && e[0] == '0');
-  }();
-  const bool max_wave = wave_ok && bpf == 1;
+  const bool max_wave = bpf == 1;
   a.mx_bpf = (p.mode == LORA_MODE_LEGACY && frame_len > 0) ? bpf : 0;
   // split evenly over the frame's blocks
   const int chunk = (int)((((frame_len + bpf - 1) / bpf) + 1) & ~int64_t(1));
@@ -1078,49 +978,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     if (prev != p.device) hipSetDevice(prev);
     return set_error(LORA_EINVAL, "batch too large");
   }
-  // Per-frame prep of one chunk: (LEGACY) frame max, then estimate + sync symbols.
   int kernels = 0;
-  auto prep = [&](const KArgs& ac, uint32_t* mb, int64_t nf, hipStream_t s) {
-    if (p.mode == LORA_MODE_LEGACY && frame_len > 0) {
-      kernels |= LORA_KERNEL_FRAME_MAX | (max_wave ? LORA_KERNEL_FRAME_MAX_WAVE : 0);
-      ProfScope ps(plan, 0, s);
-      if (max_wave)
-        hipLaunchKernelGGL(k_frame_max_wave, dim3((unsigned)((nf + 3) / 4)), dim3(256), 0, s, ac, nf, mb);
-      else
-        hipLaunchKernelGGL(k_frame_max, dim3((unsigned)(nf * bpf)), dim3(256), 0, s, ac, bpf, chunk, mb);
-    }
-    ProfScope ps(plan, 1, s);
-    kernels |= LORA_KERNEL_ESTIMATE;
-    if (!plan->use_fast || !lora::launch_est_fast(ac, nf, s)) {
-      kernels |= LORA_KERNEL_GENERIC;
-      hipLaunchKernelGGL(k_estimate, dim3((unsigned)nf), dim3(256), sizeof(cf) * plan->N, s, ac);
-    }
-  };
-  auto demod = [&](const KArgs& ac, int64_t nf, hipStream_t s) {
-    const int64_t work = nf * per;
-    if (work <= 0) return;
-    ProfScope ps(plan, 2, s);
-    kernels |= LORA_KERNEL_DEMOD;
-    if (!plan->use_fast || !lora::launch_demod_fast(ac, s0, work, s)) {
-      kernels |= LORA_KERNEL_GENERIC;
-      const int G = std::max(1, 1024 / plan->N);
-      hipLaunchKernelGGL(k_demod, dim3((unsigned)((work + G - 1) / G)), dim3(256),
-                         sizeof(cf) * G * plan->N, s, ac, G, s0, work);
-    }
-  };
-  auto chunk_args = [&](int64_t c0) {
-    KArgs ac = a;
-    ac.iq = a.iq + c0 * frame_stride;
-    ac.maxbits = a.maxbits + c0 * bpf;
-    ac.fp = a.fp + c0;
-    if (ac.syms) ac.syms = a.syms + c0 * a.sym_stride;
-    if (ac.sync) ac.sync = a.sync + c0;
-    if (ac.cfo) ac.cfo = a.cfo + c0;
-    if (ac.toff) ac.toff = a.toff + c0;
-    if (ac.max_amp) ac.max_amp = a.max_amp + c0;
-    return ac;
-  };
-  const int nchunks = (int)std::min<int64_t>(plan->max_chunks, frames / 1024);
   int rc = LORA_OK;
   if (p.mode == LORA_MODE_RAW) {
     // detector only: per-frame outputs are defined as 0
@@ -1130,74 +988,63 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     if (a.toff && e == hipSuccess) e = hipMemsetAsync(a.toff, 0, sizeof(float) * (size_t)frames, st);
     if (a.max_amp && e == hipSuccess) e = hipMemsetAsync(a.max_amp, 0, sizeof(float) * (size_t)frames, st);
     if (e != hipSuccess) rc = set_error(LORA_EIO, "hipMemsetAsync failed");
-    if (rc == LORA_OK) demod(a, frames, st);
-  } else if (nchunks <= 1) {
-    bool fused = false;
-    if (plan->use_fast && plan->fused_lds_max > 0 && p.mode == LORA_MODE_LEGACY) {
+  }
+  // Speculative single-read pipeline (LoRaDemod.cpp:59-192 reordered, results identical):
+  //   1. offset estimate on UNSCALED samples (k_est_fast<SPEC=1>), plus the maximum of the
+  //      samples outside the data-symbol windows it implies;
+  //   2. every data symbol with those offsets on unscaled samples (k_demod_fast<SPEC>),
+  //      which also reduces each window's max(|I|,|Q|) - the frame-max pass's work, from
+  //      the same read - and records the symbol's argmax margin;
+  //   3. the exact estimate from the assembled maximum (k_est_fast<SPEC=2>): outputs, sync
+  //      word, and each speculative symbol either certified (its margin exceeds the
+  //      rounding bound, so the reference's argmax is the same bin) or recomputed exactly.
+  // The IQ is read once plus symbols 0/1 twice; lora_demod_spec_recomputed() counts
+  // recomputations.  The symbol demod rotates with the hardware sine/cosine under either
+  // precision; the certification holds it to the EXACT reference.
+  const bool spec_ok = plan->spec && p.mode == LORA_MODE_LEGACY && p.osr == 1 && !a.hann && p.sf >= 6 &&
+                       total >= 3 && total - 2 + 1 <= lora::kMaxBpf;
+  if (rc == LORA_OK && spec_ok) {
+    KArgs as = a;
+    as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows
+    bool ok;
+    {
+      ProfScope ps(plan, 1, st);
+      ok = lora::launch_spec(as, frames, 0, st);
+    }
+    if (ok) {
       ProfScope ps(plan, 2, st);
-      fused = lora::launch_fused(a, frames, plan->fused_lds_max, st);
+      ok = lora::launch_spec(as, frames, 1, st);
     }
-    if (fused) kernels |= LORA_KERNEL_FUSED;
-    // Speculative single-read pipeline (LoRaDemod.cpp:59-192 reordered, results identical):
-    //   1. offset estimate on UNSCALED samples (k_est_fast<SPEC=1>), plus the maximum of the
-    //      samples outside the data-symbol windows it implies;
-    //   2. every data symbol with those offsets on unscaled samples (k_demod_fast<SPEC>),
-    //      which also reduces each window's max(|I|,|Q|) - the frame-max pass's work, from
-    //      the same read - and records the symbol's argmax margin;
-    //   3. the exact estimate from the assembled maximum (k_est_fast<SPEC=2>): outputs, sync
-    //      word, and each speculative symbol either certified (its margin exceeds the
-    //      rounding bound, so the reference's argmax is the same bin) or recomputed exactly.
-    // A frame that needs no rescaling (max <= 1) is exact as computed.  The IQ is read once
-    // plus symbols 0/1 twice; lora_demod_spec_recomputed() counts recomputations.  Under
-    // LORA_PRECISION_FAST step 2 rotates with the hardware sine/cosine and step 3 certifies
-    // those symbols against the EXACT reference (a wider bound), so rescaled frames come
-    // out exact; unscaled frames keep the FAST symbols, as the three-launch path has them.
-    const bool spec_ok = !fused && plan->use_fast && plan->spec && p.mode == LORA_MODE_LEGACY && p.osr == 1 &&
-                         !a.hann && !a.ablate && p.sf >= 6 && total >= 3 &&
-                         total - 2 + 1 <= lora::kMaxBpf;
-    bool spec_done = false;
-    if (spec_ok) {
-      KArgs as = a;
-      as.spec_hw = plan->spec_hw;
-      as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows
-      as.maxbits = maxbits;
-      bool ok;
-      {
-        ProfScope ps(plan, 1, st);
-        ok = lora::launch_spec(as, frames, 0, st);
+    if (ok) {
+      ProfScope ps(plan, 1, st);
+      ok = lora::launch_spec(as, frames, 2, st);
+    }
+    if (!ok) rc = set_error(LORA_EIO, "speculative pipeline launch failed");
+    kernels |= LORA_KERNEL_SPEC | LORA_KERNEL_ESTIMATE | LORA_KERNEL_DEMOD;
+  } else if (rc == LORA_OK) {
+    // three launches: (LEGACY) frame max, estimate + sync symbols, symbol demod
+    if (p.mode == LORA_MODE_LEGACY && frame_len > 0) {
+      kernels |= LORA_KERNEL_FRAME_MAX | (max_wave ? LORA_KERNEL_FRAME_MAX_WAVE : 0);
+      ProfScope ps(plan, 0, st);
+      if (max_wave)
+        hipLaunchKernelGGL(k_frame_max_wave, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, st, a, frames,
+                           maxbits);
+      else
+        hipLaunchKernelGGL(k_frame_max, dim3((unsigned)(frames * bpf)), dim3(256), 0, st, a, bpf, chunk, maxbits);
+    }
+    if (p.mode != LORA_MODE_RAW) {
+      ProfScope ps(plan, 1, st);
+      kernels |= LORA_KERNEL_ESTIMATE;
+      if (!lora::launch_est_fast(a, frames, st)) {
+        kernels |= LORA_KERNEL_GENERIC;
+        hipLaunchKernelGGL(k_estimate, dim3((unsigned)frames), dim3(256), sizeof(cf) * plan->N, st, a);
       }
-      if (ok) {
-        ProfScope ps(plan, 2, st);
-        ok = lora::launch_spec(as, frames, 1, st);
-      }
-      if (ok) {
-        ProfScope ps(plan, 1, st);
-        ok = lora::launch_spec(as, frames, 2, st);
-      }
-      if (!ok) rc = set_error(LORA_EIO, "speculative pipeline launch failed");
-      spec_done = true;
-      kernels |= LORA_KERNEL_SPEC | LORA_KERNEL_ESTIMATE | LORA_KERNEL_DEMOD;
     }
-    if (!fused && !spec_done) {
-      prep(a, maxbits, frames, st);
-      demod(a, frames, st);
-    }
-  } else {
-    // fork: aux waits for the caller's prior work, runs every chunk's prep; the
-    // caller's stream joins chunk by chunk before each demod (capturable pattern).
-    hipStream_t ax = plan->aux;
-    hipEventRecord(plan->ev_fork, st);
-    hipStreamWaitEvent(ax, plan->ev_fork, 0);
-    const int64_t fpc = (frames + nchunks - 1) / nchunks;
-    for (int c = 0; c < nchunks && rc == LORA_OK; ++c) {
-      const int64_t c0 = c * fpc, nf = std::min(fpc, frames - c0);
-      if (nf > 0) prep(chunk_args(c0), maxbits + c0 * bpf, nf, ax);
-      hipEventRecord(plan->ev_chunk[c], ax);
-    }
-    for (int c = 0; c < nchunks && rc == LORA_OK; ++c) {
-      const int64_t c0 = c * fpc, nf = std::min(fpc, frames - c0);
-      hipStreamWaitEvent(st, plan->ev_chunk[c], 0);
-      if (nf > 0) demod(chunk_args(c0), nf, st);
+    const int64_t work = frames * per;
+    if (work > 0) {
+      ProfScope ps(plan, 2, st);
+      kernels |= LORA_KERNEL_DEMOD;
+      if (!lora::launch_demod_fast(a, s0, work, st)) rc = set_error(LORA_EIO, "symbol demod launch failed");
     }
   }
   if (plan->prof_calls < plan->prof_max) ++plan->prof_calls;

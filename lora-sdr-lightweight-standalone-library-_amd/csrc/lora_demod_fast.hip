@@ -230,17 +230,7 @@ __device__ __forceinline__ void pass_regs_T2(cf* x, int k, const cf* __restrict_
 
 // The other lanes' share of one pass: read R points from LDS, run the stages,
 // either write them back or fold them into the argmax key.
-#ifndef LORA_SPEC_ABL
-#define LORA_SPEC_ABL 0  // A/B only: 1 = skip the speculative extras (results invalid)
-#endif
-#ifndef LORA_SPEC_ABLX
-#define LORA_SPEC_ABLX 0  // A/B only: ablation bits (ABL below) for the speculative demod
-#endif
-
-// XA: profiling-only ablation bits of the speculative kernel (LORA_SPEC_ABLX, results
-// invalid): 16 = no LDS reads (the lane's own values stand in), 32 = one twiddle load
-// per group instead of one per butterfly input.
-template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false, int XA = 0, bool PAIR = false>
+template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false, bool PAIR = false>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
                                          uint64_t& key, const cf* __restrict__ twT = nullptr,
                                          float* second = nullptr) {
@@ -251,20 +241,8 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     const int k = GI % MA, cc = GI / MA;
     cf* xs = x + gg * R;
     const cf* rb = row + lds_slot<SF>(cc * MA * R + k);  // k < MA, MA*u: disjoint bits
-    if constexpr (!(XA & 16)) {
 #pragma unroll
-      for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
-    }
-    if constexpr ((XA & 32) && (R == 4 || R == 16)) {
-      const cf w = twT ? twT[k] : tw[k];
-#pragma unroll
-      for (int blk = 0; blk < R; blk += 4) bfly4<FMA>(xs[blk], xs[blk + 1], xs[blk + 2], xs[blk + 3], w, w, w);
-      if constexpr (R == 16) {
-#pragma unroll
-        for (int uu = 0; uu < 4; ++uu) bfly4<FMA>(xs[uu], xs[uu + 4], xs[uu + 8], xs[uu + 12], w, w, w);
-      }
-      continue;
-    }
+    for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
     if constexpr (R == 4 || R == 16) {
       if (twT) {
         if constexpr (PAIR)
@@ -341,13 +319,13 @@ __device__ __forceinline__ void sym_base(int s, int step, int64_t frame_len, int
 // and apply what precedes the rotation: KIND 0 raw (API estimate, phy.cpp:91-99),
 // KIND 1 LEGACY (caller dechirp, e2e_chain_test.cpp:88-93, then normalisation,
 // LoRaDemod.cpp:68-77), KIND 2 API down-chirp (phy.cpp:216-225).
-template <int SF, int ABL, bool PAIRD = false>
+template <int SF, bool PAIRD = false>
 __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restrict__ x, int l,
                                               int osr, int step, int cg, int kind, bool dech,
                                               float scale, cf* in) {
   using G = Geo<SF>;
   constexpr int T = G::T, P = G::P;
-  if constexpr (PAIRD && P == 16 && !(ABL & 12)) {
+  if constexpr (PAIRD && P == 16) {
     // speculative demod, LEGACY osr 1 with the fused dechirp: the table values two per
     // 16-byte load from KArgs::downP (same values, same products)
     const cf* __restrict__ xl = x + l;
@@ -377,12 +355,7 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
   // T*q (times osr) from it, which fold into the loads' immediate offsets at osr 1.
   const cf* __restrict__ xl = x + (int64_t)l * osr;
 #pragma unroll
-  for (int q = 0; q < P; ++q) {
-    if (ABL & 4)
-      in[q] = cf{0.0f, 0.0f};
-    else
-      in[q] = xl[(int64_t)(T * q) * osr];
-  }
+  for (int q = 0; q < P; ++q) in[q] = xl[(int64_t)(T * q) * osr];
   if (kind == 2) {
     const cf* __restrict__ dl = a.down1 + l;
 #pragma unroll
@@ -391,14 +364,8 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
     if (dech) {
       // caller-side dechirp phase cg + i*osr < 2*step: the doubled table needs no wrap
       const cf* __restrict__ dl = a.down + cg + l * osr;
-      if (ABL & 8) {  // profiling only: one table value for every point
-        const cf d0 = dl[0];
 #pragma unroll
-        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], d0);
-      } else {
-#pragma unroll
-        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[(T * q) * osr]);
-      }
+      for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[(T * q) * osr]);
     }
 #pragma unroll
     for (int q = 0; q < P; ++q) in[q] = cscale(in[q], scale);
@@ -424,20 +391,16 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 #ifndef LORA_TWB_PAIR
 #define LORA_TWB_PAIR 1  // ... and pass B's twiddles in slot pairs (KArgs::twTB2)
 #endif
-#ifndef LORA_ROT_REC
-#define LORA_ROT_REC 1  // certified demod: rotation factors by recurrence (0: one sin/cos pair per point)
-#endif
-template <int SF, bool ROT, int ABL, bool FAST = false, bool FMA = false>
+template <int SF, bool ROT, bool FAST = false, bool FMA = false>
 __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, float rate,
                                              bool hann, const float* __restrict__ win, int l) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
-  if constexpr (FAST && ROT && !(ABL & 1)) {
+  if constexpr (FAST && ROT) {
     // LORA_PRECISION_FAST: the same fp32 phase (LoRaDemod.cpp:151-154), then the hardware
     // sine/cosine on its fractional revolution (v_fract, v_sin_f32, v_cos_f32) instead of
     // glibc's sincosf - not bit-exact (include/lora_mi355x.h states the tolerance).
     constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
-#if LORA_ROT_REC
     if constexpr (FMA) {
       // Certified speculative demod: the lane's points i = l + T*q are T apart, so the
       // factor of point q is e^{i(ph_l + q*rate*T)}: one hardware sin/cos pair for the
@@ -459,7 +422,6 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
       }
       return;
     }
-#endif
 #pragma unroll
     for (int q = 0; q < P; ++q) {
       const float ph = start + rate * (float)(l + T * q);
@@ -470,11 +432,11 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
     }
     return;
   }
-  if (!ROT || (ABL & 1)) {
+  if constexpr (!ROT) {
 #pragma unroll
     for (int q = 0; q < P; ++q) {
       cf v = in[q];
-      if (hann && !(ABL & 1)) v = cscale(v, win[l + T * q]);
+      if (hann) v = cscale(v, win[l + T * q]);
       z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
     }
     return;
@@ -514,16 +476,14 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
 // FFT of the symbol held as pass-1 inputs in z (T lanes x P points) and the lane's
 // argmax key.  KEEP: leave the spectrum in natural order in `row` (padded address
 // paddr(bin)) for the estimate's neighbour bins; NPASS == 1 keeps it in z.
-template <int SF, bool KEEP, int ABL, bool FMA = false, bool TWL = false>
+template <int SF, bool KEEP, bool FMA = false, bool TWL = false>
 __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr,
                                             const cf* twl = nullptr) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
   constexpr bool WL = G::WAVE_LOCAL;
-  if (!(ABL & 2)) {
 #pragma unroll
-    for (int h = 0; h < G::G1; ++h) pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP, FMA>(z + h * R1, 0, a.tw);
-  }
+  for (int h = 0; h < G::G1; ++h) pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP, FMA>(z + h * R1, 0, a.tw);
   uint64_t key = 0;
   if constexpr (G::NPASS == 1) {
     float best = 0.0f;
@@ -545,24 +505,21 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
     for (int h = 0; h < G::G1; ++h)
 #pragma unroll
       for (int u = 0; u < R1; ++u)
-        if (!(ABL & 16)) row[lds_slot<SF>(c[h] * R1) + u] = z[h * R1 + u];  // u < 16
-    if (!(ABL & 16)) block_sync<WL>();
+        row[lds_slot<SF>(c[h] * R1) + u] = z[h * R1 + u];  // u < 16
+    block_sync<WL>();
     constexpr int RL = G::NPASS == 2 ? G::RA : G::RB;   // last pass span
     constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
-    constexpr int XA = ABL & 48;
     // TWL: pass A's slot-major twiddles from the workgroup's LDS copy (k_demod_fast)
     const cf* twA = TWL ? twl : a.twTA;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA, XA>(row, z, l, a.tw, key, twA, second);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA>(row, z, l, a.tw, key, twA, second);
     } else {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA, XA>(row, z, l, a.tw, key, twA);
-      if (!(ABL & 16)) {
-        block_sync<WL>();
-        write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
-        block_sync<WL>();
-      }
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA>(row, z, l, a.tw, key, twA);
+      block_sync<WL>();
+      write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
+      block_sync<WL>();
       // TWL (speculative demod): pass B's twiddles two per 16-byte load (KArgs::twTB2)
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, XA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR>(
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR>(
           row, z, l, a.tw, key, ((TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
     }
     if constexpr (KEEP) {
@@ -682,9 +639,6 @@ __device__ __forceinline__ void group_reduce2(float& a, float& b, int tid, float
 // MODE 1: LEGACY on already-dechirped input, osr 1, no window (lora_demodulate's own
 //         contract); MODE 2: every other LEGACY / API configuration, flags read at run
 //         time; MODE 3: RAW (detector only: no normalisation, estimate or rotation).
-// ABL: profiling-only ablation mask (LORA_MI355X_ABLATE; results are NOT valid):
-// 1 = identity rotation instead of sincosf, 2 = skip the pass-1 FFT stages, 4 = skip
-// the HBM loads, 8 = one dechirp-table value per lane instead of one per point.
 // Register budget: 4 waves per SIMD (<= 128 VGPRs) for SF >= 6 - the LDS rows allow
 // 4 workgroups per CU, so this is the occupancy ceiling.  With scalar fp32 the kernels
 // need 115-128 VGPRs and fit without spilling; SF <= 5 keeps a whole symbol per lane
@@ -714,14 +668,13 @@ constexpr int demod_twl_entries() {
 // offsets (fp_spec) on unscaled samples, and per data symbol (spec_marg, one 8-byte
 // store) the margin |X1| - |X2| between the top bin and the runner-up and the window's
 // max(|I|,|Q|), which k_est_fast<SPEC = 2> uses to normalise, certify or recompute.
-template <int SF, int MODE, int ABL = 0, bool FAST = false, bool SPEC = false>
+template <int SF, int MODE, bool FAST = false, bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
   constexpr bool RAW = MODE == 3;
   constexpr bool DYN = MODE >= 2;
-  constexpr int AB = ABL | (SPEC ? LORA_SPEC_ABLX : 0);  // profiling-only ablation bits
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint64_t red[4];
   cf* rows = reinterpret_cast<cf*>(smem);
@@ -763,9 +716,9 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   }
   cf in[P], z[P];
   if (SPEC && LORA_DECH_PAIR && MODE == 0 && a.downP)  // the speculative demod's scale is 1
-    gather_points<SF, AB, true>(a, x, l, 1, N, cg, 1, true, 1.0f, in);
+    gather_points<SF, true>(a, x, l, 1, N, cg, 1, true, 1.0f, in);
   else
-    gather_points<SF, AB>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
+    gather_points<SF>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
   if constexpr (NTW > 0) {
     if (tid < NTW) twl[tid] = tv;
     // wave-local kernels have no workgroup barrier before pass A; the others' first one
@@ -773,18 +726,18 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
     if constexpr (G::WAVE_LOCAL) __syncthreads();
   }
   float pm = 0.0f;
-  if constexpr (SPEC && !LORA_SPEC_ABL) {  // the window's dechirped, unscaled samples (scale is 1 here)
+  if constexpr (SPEC) {  // the window's dechirped, unscaled samples (scale is 1 here)
 #pragma unroll
     for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
   }
-  rotate_place<SF, !RAW, AB, FAST, FMA>(in, z, start, p.rate, hann, a.win, l);
-  if constexpr (SPEC && !LORA_SPEC_ABL) asm volatile("" : "+v"(pm));
+  rotate_place<SF, !RAW, FAST, FMA>(in, z, start, p.rate, hann, a.win, l);
+  if constexpr (SPEC) asm volatile("" : "+v"(pm));
   float sec = 0.0f;
-  const uint64_t lkey = fft_key<SF, false, AB, FMA, (NTW > 0)>(z, rows + (size_t)g * rowc, l, a,
-                                                               SPEC && !LORA_SPEC_ABL ? &sec : nullptr, twl);
+  const uint64_t lkey =
+      fft_key<SF, false, FMA, (NTW > 0)>(z, rows + (size_t)g * rowc, l, a, SPEC ? &sec : nullptr, twl);
   const uint64_t key = symbol_key<SF>(lkey, tid, red);
   if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + (s - s0)] = (uint16_t)key_index(key);
-  if constexpr (SPEC && !LORA_SPEC_ABL) {
+  if constexpr (SPEC) {
     // runner-up over the symbol: the top lane offers its own runner-up, the others their best
     float r2 = lkey == key ? sec : key_value(lkey);
     group_reduce2<SF>(r2, pm, tid, reinterpret_cast<float*>(smem + 64));
@@ -874,12 +827,9 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   const int scaled = maxv > 1.0f;
   const float scale = scaled ? 1.0f / maxv : 1.0f;
   if constexpr (SPEC == 2) {
-    // max <= 1: no rescaling, so the pre-pass estimate, its sync word and every
-    // speculative symbol are already the reference's (identical inputs and arithmetic) -
-    // unless the symbols were rotated with the hardware sine/cosine (spec_hw), in which
-    // case the frame goes through the certification below like a rescaled one.
-    // Frame-uniform exit: T-lane groups are whole waves or lie within one, and waves that
-    // have ended drop out of the other frames' later s_barriers.
+    // max <= 1: no rescaling, so the pre-pass estimate and its sync word are already the
+    // reference's (identical inputs and arithmetic); the symbols, rotated with the
+    // hardware sine/cosine, go through the certification below like a rescaled frame's.
     if (!scaled) {
       if (l == 0 && valid) {
         const FrameParams qs = a.fp_spec[f];
@@ -889,7 +839,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         if (a.max_amp) a.max_amp[f] = maxv;
         if (a.sync) a.sync[f] = (uint8_t)qs.pad0;
       }
-      if (!a.spec_hw) return;
     }
   }
   // The frame's exact offsets: estimated below, or for an unscaled frame of the
@@ -915,15 +864,15 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       unsigned bt[2] = {0, 0};
       cf bbin[2] = {cf{0.0f, 0.0f}, cf{0.0f, 0.0f}};
       for (int t = 0; t < osr; ++t) {
-        gather_points<SF, 0>(a, x + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in);
-        gather_points<SF, 0>(a, x + (int64_t)step + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in1);
+        gather_points<SF>(a, x + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in);
+        gather_points<SF>(a, x + (int64_t)step + t, l, osr, step, t, legacy ? 1 : 0, dech, scale, in1);
         if constexpr (SPEC == 1) {
 #pragma unroll
           for (int q = 0; q < P; ++q) mo = amax3(amax3(mo, in[q]), in1[q]);
           asm volatile("" : "+v"(mo));
         }
-        rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
-        rotate_place<SF, false, 0>(in1, z1, 0.0f, 0.0f, hann, a.win, l);
+        rotate_place<SF, false>(in, z, 0.0f, 0.0f, hann, a.win, l);
+        rotate_place<SF, false>(in1, z1, 0.0f, 0.0f, hann, a.win, l);
         uint64_t key[2];
         fft_key2<SF, true>(z, z1, row, row1, l, a, key[0], key[1]);
         key[0] = group_max(key[0], T);
@@ -972,15 +921,15 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       unsigned best_t = 0;
       cf best_bin = {0.0f, 0.0f};
       for (int t = 0; t < osr; ++t) {
-        gather_points<SF, 0>(a, x + (int64_t)s * step + t, l, osr, step, t, legacy ? 1 : 0, dech,
+        gather_points<SF>(a, x + (int64_t)s * step + t, l, osr, step, t, legacy ? 1 : 0, dech,
                              scale, in);
         if constexpr (SPEC == 1) {
 #pragma unroll
           for (int q = 0; q < P; ++q) mo = amax3(mo, in[q]);
           asm volatile("" : "+v"(mo));
         }
-        rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, hann, a.win, l);
-        uint64_t key = fft_key<SF, true, 0>(z, row, l, a);
+        rotate_place<SF, false>(in, z, 0.0f, 0.0f, hann, a.win, l);
+        uint64_t key = fft_key<SF, true>(z, row, l, a);
         key = symbol_key<SF>(key, tid, red);
         if (l == 0) {
           const uint32_t idx = key_index(key);
@@ -1097,10 +1046,10 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       const float st0 = q.rate * ((float)((uint32_t)0 * (uint32_t)N) + (float)q.t_off / (float)osr);
       const float st1 = q.rate * ((float)((uint32_t)1 * (uint32_t)N) + (float)q.t_off / (float)osr);
       const float sc = (legacy && q.scaled) ? q.scale : 1.0f;
-      gather_points<SF, 0>(a, x + base0, l, osr, step, cg0, legacy ? 1 : 2, dech, sc, in);
-      gather_points<SF, 0>(a, x + base1, l, osr, step, cg1, legacy ? 1 : 2, dech, sc, in1);
-      rotate_place<SF, true, 0>(in, z, st0, q.rate, hann, a.win, l);
-      rotate_place<SF, true, 0>(in1, z1, st1, q.rate, hann, a.win, l);
+      gather_points<SF>(a, x + base0, l, osr, step, cg0, legacy ? 1 : 2, dech, sc, in);
+      gather_points<SF>(a, x + base1, l, osr, step, cg1, legacy ? 1 : 2, dech, sc, in1);
+      rotate_place<SF, true>(in, z, st0, q.rate, hann, a.win, l);
+      rotate_place<SF, true>(in1, z1, st1, q.rate, hann, a.win, l);
       uint64_t k0, k1;
       fft_key2<SF, false>(z, z1, row, row1, l, a, k0, k1);
       sw[0] = key_index(group_max(k0, T));
@@ -1111,10 +1060,10 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       int cg;
       sym_base(s, step, a.frame_len, q.t_off, base, cg);
       const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
-      gather_points<SF, 0>(a, x + base, l, osr, step, cg, legacy ? 1 : 2, dech,
+      gather_points<SF>(a, x + base, l, osr, step, cg, legacy ? 1 : 2, dech,
                            (legacy && q.scaled) ? q.scale : 1.0f, in);
-      rotate_place<SF, true, 0>(in, z, start, q.rate, hann, a.win, l);
-      uint64_t key = fft_key<SF, false, 0>(z, row, l, a);
+      rotate_place<SF, true>(in, z, start, q.rate, hann, a.win, l);
+      uint64_t key = fft_key<SF, false>(z, row, l, a);
       key = symbol_key<SF>(key, tid, red);
       sw[s] = key_index(key);
       block_sync<G::WAVE_LOCAL>();
@@ -1163,7 +1112,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
           // sum_i |y_i| <= sum_i (|re_i| + |im_i|) <= 2 N max(|re|, |im|) over the window
           const double n1 = 2.0 * N * (double)v.y;
           const double L = (double)(2 + j) * N + tabs + N;  // |phase argument| scale of symbol 2+j
-          // Hardware rotation (spec_hw, LORA_PRECISION_FAST): the demod rotated by
+          // Hardware rotation: the demod rotated by
           // v_sin/v_cos_f32 of fract(fl(ph * fl(1/2pi))) instead of glibc sincosf(ph): the
           // argument's two roundings move the angle by <= 2 eps |ph| rad, and the unit itself
           // is within 1.26e-7 of sin/cos(2 pi r) for every fp32 r in [0, 1) (measured
@@ -1172,14 +1121,14 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
           // complex products with fused multiply-adds: one rounding where the reference has
           // two, so E bounds its FFT and products as well.  Certified against the exact
           // reference like every other symbol.
-          // With LORA_ROT_REC the demod takes one such factor r0 per lane (its first point)
+          // The demod takes one such factor r0 per lane (its first point)
           // and one w for the step rate*T, then r_{q+1} = fma-product(r_q, w) for the lane's
           // P = 16 points: |r_q - e^{i phi_q}| <= E_0 + q (e_w + 2 sqrt2 eps), with
           // E_0 <= 2 eps |ph_0| + sqrt2 * 1.26e-7 and e_w <= 2 eps |rate T| + sqrt2 * 1.26e-7
           // (|r|, |w| within 3e-6 of 1), so every factor is off by < 2 eps rmax L + 5.4e-6
           // (|ph_0| + 15 |rate| T <= rmax L); doubled here.
-          const double hwd = LORA_ROT_REC ? 1.1e-5 : 4e-7;
-          const double fastd = (a.fast_rot || a.spec_hw) ? 4.0 * eps * rmax * L + hwd : 0.0;
+          const double hwd = 1.1e-5;
+          const double fastd = 4.0 * eps * rmax * L + hwd;
           const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E + fastd);
           if (!(same_t && (double)d > 4.0 * B)) bad |= 1u << i;
         }
@@ -1201,9 +1150,9 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         int cg;
         sym_base(s, step, a.frame_len, q.t_off, base, cg);
         const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
-        gather_points<SF, 0>(a, x + base, l, osr, step, cg, 1, dech, q.scaled ? q.scale : 1.0f, in);
-        rotate_place<SF, true, 0>(in, z, start, q.rate, hann, a.win, l);
-        uint64_t key = fft_key<SF, false, 0>(z, row, l, a);
+        gather_points<SF>(a, x + base, l, osr, step, cg, 1, dech, q.scaled ? q.scale : 1.0f, in);
+        rotate_place<SF, true>(in, z, start, q.rate, hann, a.win, l);
+        uint64_t key = fft_key<SF, false>(z, row, l, a);
         key = symbol_key<SF>(key, tid, red);
         if (l == 0 && valid) {
           if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)key_index(key);
@@ -1213,976 +1162,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       }
     }
   }
-}
-
-// ---- frame-resident pipeline: one HBM read per sample --------------------------------
-// LEGACY, osr 1, no window (MODE 0: fused caller dechirp, MODE 1: dechirped input), SF
-// 6-8, frames that fit LDS.  One workgroup per frame:
-//   load      the frame streams HBM -> registers once (16-byte nontemporal loads), is
-//             dechirped (e2e_chain_test.cpp:88-93), reduced to max(|I|,|Q|)
-//             (LoRaDemod.cpp:59-67) and stored to LDS as rows of ROW = lds_row<SF>()
-//             complex values per symbol (sample j at row j>>SF, column j&(N-1));
-//   estimate  one T-lane group: symbols 0 and 1 scaled (LoRaDemod.cpp:68-77), the
-//             offset estimate (:79-135) and the sync symbols (:165-168, 177-192), as
-//             k_est_fast, reading LDS instead of HBM (one scratch row after the frame);
-//   demod     rounds of BLOCK/T data symbols read from LDS with the t_off rule
-//             (:142-149), then each symbol's transposes run in place in its own row.
-//             The rows a round reads are never rows an earlier round wrote: with
-//             t_off >= 0 a window reaches into the next row, so rounds go up; with
-//             t_off < 0 into the previous row, so rounds go down.  One barrier per
-//             round separates its reads from its in-place writes.
-// Two workgroups share a CU (frame <= ~78 KB), so one frame's load overlaps the other's
-// arithmetic; the separate frame-max pass and its second read of the IQ are gone.
-template <int SF>
-__device__ __forceinline__ void lds_points(const cf* __restrict__ frame, int s, int e, int l, float scale,
-                                           cf* in) {
-  using G = Geo<SF>;
-  constexpr int N = G::N, T = G::T, P = G::P, ROW = lds_row<SF>(), PADC = ROW - N;
-  // point q of lane l: frame sample s*N + e + l + T*q (|e| < N), row-crossing folded in
-  const cf* b = frame + s * ROW + e + l;
-  if (__all(e == 0)) {
-#pragma unroll
-    for (int q = 0; q < P; ++q) in[q] = cscale(b[T * q], scale);
-  } else {
-    const int p0 = e + l;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const int p = p0 + T * q;
-      const int c = p >= N ? PADC : (p < 0 ? -PADC : 0);
-      in[q] = cscale(b[T * q + c], scale);
-    }
-  }
-}
-
-#ifdef LORA_FUSED_TIMING
-// Development instrumentation (never in the product build): per workgroup and frame
-// iteration (first 16), s_memrealtime (100 MHz) stamps at the phase boundaries plus the hardware id.
-__device__ unsigned long long g_fused_dbg[2048 * 16 * 8];
-#define FSTAMP(it, k)                                                                          \
-  do {                                                                                         \
-    if (threadIdx.x == 0 && blockIdx.x < 2048 && (it) < 16)                                    \
-      g_fused_dbg[((size_t)blockIdx.x * 16 + (it)) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define FSTAMP(it, k) \
-  do {                \
-  } while (0)
-#endif
-
-// LDS bytes of the FFT tables k_frame_fused keeps next to the frame: tw (N), the pass-A
-// slot-major twiddles (15 or 3 slots x MA_A) and the leaf order (N x u16).
-template <int SF>
-struct FusedTables {
-  static constexpr int TWT = (Geo<SF>::RA == 16 ? 15 : 3) * Geo<SF>::MA_A;
-  static constexpr int BYTES = ((8 * (Geo<SF>::N + TWT) + 2 * Geo<SF>::N) + 15) & ~15;
-};
-
-// Estimate candidate of one symbol (LoRaDemod.cpp:86-110 with osr 1), handed from the
-// group that transformed it to thread 0.
-struct EstCand {
-  cf bin;
-  float fi;
-  uint32_t idx, take, pad;
-};
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not
-// for its global loads and stores (__syncthreads' fence also drains those: the output
-// stores and the IQ loads in flight would stall every barrier).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// One frame of k_frame_fused.
-template <int SF, int MODE, bool FAST>
-__device__ __forceinline__ LORA_SCALAR_FP32 void fused_frame(const KArgs& a, int nrows, int64_t f,
-                                                                      unsigned char* smem, float* wmax,
-                                                                      FrameParams& sp, EstCand* ec, uint32_t* swl,
-                                                                      int it) {
-  using G = Geo<SF>;
-  constexpr int N = G::N, T = G::T, P = G::P, ROW = lds_row<SF>();
-  constexpr bool DECH = MODE == 0;
-  cf* frame = reinterpret_cast<cf*>(smem);
-  cf* er = frame + nrows * ROW;  // two scratch rows: the estimate / sync transforms of symbols 0, 1
-  // The FFT tables in LDS (copied while the frame streams in): the transforms' twiddle and
-  // leaf-order reads are then LDS reads, off the latency chain of the estimate and sync
-  // symbols and off the vector-memory path of the data symbols.
-  cf* ltw = er + 2 * ROW;
-  cf* ltwT = ltw + N;
-  uint16_t* lrev = reinterpret_cast<uint16_t*>(ltwT + FusedTables<SF>::TWT);
-  KArgs b = a;
-  b.tw = ltw;
-  b.twTA = a.twTA ? ltwT : nullptr;
-  b.rev = lrev;
-  const int nthr = blockDim.x;
-  const int len = (int)a.frame_len;
-  for (int i = threadIdx.x; i < N; i += nthr) {
-    ltw[i] = a.tw[i];
-    lrev[i] = a.rev[i];
-  }
-  if (a.twTA)
-    for (int i = threadIdx.x; i < FusedTables<SF>::TWT; i += nthr) ltwT[i] = a.twTA[i];
-  {
-    // Lane indices from an opaque per-frame copy of threadIdx.x: otherwise the
-    // frame-invariant lane addresses of every phase are hoisted out of this loop and
-    // kept live across it (spilled).
-    int tid = threadIdx.x;
-    asm volatile("" : "+v"(tid));
-    const int wv = tid >> 6;
-    const int g = tid / T;
-    const int l = tid % T;
-    const bool est_lane = wv < 2 && (tid & 63) < T;  // group 0 of waves 0 and 1
-    const cf* __restrict__ x = a.iq + f * a.frame_stride;
-    FSTAMP(it, 0);
-#ifdef LORA_FUSED_TIMING
-    if (threadIdx.x == 0 && blockIdx.x < 2048 && it < 16) {
-      unsigned hw;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      g_fused_dbg[((size_t)blockIdx.x * 16 + it) * 8 + 7] = ((unsigned long long)xcc << 32) | hw;
-    }
-#endif
-    // ---- load: HBM -> (dechirp) -> max -> LDS ----
-    float m = 0.0f;
-    {
-#ifndef LORA_FUSED_KB
-#define LORA_FUSED_KB 9
-#endif
-      constexpr int KB = LORA_FUSED_KB;
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      const int p1 = len >> 1;
-      for (int pb = tid; pb < p1; pb += KB * nthr) {
-        f4v q[KB];
-#pragma unroll
-        for (int k = 0; k < KB; ++k) {
-          const int pr = pb + k * nthr;
-          q[k] = pr < p1 ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(x) + pr)
-                         : f4v{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-        f4v w[KB];
-        if constexpr (DECH) {
-#pragma unroll
-          for (int k = 0; k < KB; ++k)  // table phase of an even sample is even: 16-B aligned
-            w[k] = *reinterpret_cast<const f4v*>(a.down + ((2 * (pb + k * nthr)) & (N - 1)));
-        }
-#pragma unroll
-        for (int k = 0; k < KB; ++k) {
-          const int pr = pb + k * nthr;
-          cf v0{q[k][0], q[k][1]}, v1{q[k][2], q[k][3]};
-          if constexpr (DECH) {
-            v0 = cmul(v0, cf{w[k][0], w[k][1]});
-            v1 = cmul(v1, cf{w[k][2], w[k][3]});
-          }
-          m = fmaxf(m, fmaxf(fmaxf(fabsf(v0.re), fabsf(v0.im)), fmaxf(fabsf(v1.re), fabsf(v1.im))));
-          if (pr < p1) {
-            const int j = 2 * pr;
-            *reinterpret_cast<f4v*>(frame + (j >> SF) * ROW + (j & (N - 1))) = f4v{v0.re, v0.im, v1.re, v1.im};
-          }
-        }
-      }
-      if ((len & 1) && tid == 0) {  // odd frame length: the last sample
-        const int j = len - 1;
-        cf v = x[j];
-        if constexpr (DECH) v = cmul(v, a.down[j & (N - 1)]);
-        m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
-        frame[(j >> SF) * ROW + (j & (N - 1))] = v;
-      }
-    }
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    if ((tid & 63) == 0) wmax[wv] = m;
-    lds_barrier();
-    FSTAMP(it, 1);
-    float maxv = wmax[0];
-    for (int w = 1; w < (nthr >> 6); ++w) maxv = fmaxf(maxv, wmax[w]);
-    const int scaled = maxv > 1.0f;
-    const float scale = scaled ? 1.0f / maxv : 1.0f;  // LoRaDemod.cpp:68-77
-
-    // ---- offset estimate: symbol w on group 0 of wave w (w = 0, 1), in parallel ----
-#ifdef LORA_FUSED_NOEST  // profiling ablation (results invalid): no estimate / sync
-    if (tid == 0) sp = FrameParams{0.0f, 0.0f, 0.0f, scale, 0, scaled, 0, 0};
-    if (false) {
-#else
-    if (est_lane) {
-#endif
-      cf in[P], z[P];
-      cf* row = er + wv * ROW;
-      lds_points<SF>(frame, wv, 0, l, scale, in);
-      rotate_place<SF, false, 0>(in, z, 0.0f, 0.0f, false, nullptr, l);
-      const uint64_t key = group_max(fft_key<SF, true, 0>(z, row, l, b), T);
-      if (l == 0) {
-        const uint32_t idx = key_index(key);
-        const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
-        float pw, fi;
-        detect_tail(key_value(key), row[lds_slot<SF>((int)im1)], row[lds_slot<SF>((int)ip1)], a.power_scale, &pw,
-                    &fi);
-        // one phase (osr 1): the candidate is kept iff p > best_p = -1e30 (LoRaDemod.cpp:
-        // 87,101), else the defaults (index 0, fIndex 0, bin 0) stand
-        EstCand c;
-        c.take = pw > -1e30f;
-        c.idx = c.take ? idx : 0u;
-        c.fi = c.take ? fi : 0.0f;
-        c.bin = c.take ? row[lds_slot<SF>((int)idx)] : cf{0.0f, 0.0f};
-        c.pad = 0;
-        ec[wv] = c;
-      }
-    }
-    lds_barrier();
-    FSTAMP(it, 2);
-    if (tid == 0) {  // LoRaDemod.cpp:111-138, symbols in order
-      float sum_index = 0.0f, phase_diff = 0.0f, prev_phase = 0.0f;
-#ifndef LORA_FUSED_NOEST
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const EstCand c = ec[s];
-        sum_index += (float)c.idx + c.fi;  // best_t = 0
-        const float phase = lm_atan2f(c.bin.im, c.bin.re);
-        if (s > 0) {
-          float d = phase - prev_phase;
-          while (d > PI_F) d -= 2.0f * PI_F;
-          while (d < -PI_F) d += 2.0f * PI_F;
-          phase_diff += d;
-        }
-        prev_phase = phase;
-      }
-#endif
-      const float avg_index = sum_index / 2.0f;
-      const float cfo_coarse = avg_index / (float)N;
-      const float cfo_fine = (phase_diff / 1.0f) / (2.0f * PI_F * (float)N);
-      const float cfo = cfo_coarse + cfo_fine;
-      const float frac = avg_index - floorf(avg_index + 0.5f);
-      const float toff = 0.0f / 2.0f - frac * (float)N * 1.0f;  // avg_t = sum_t / 2 = 0
-      FrameParams q;
-      q.cfo = cfo;
-      q.toff = toff;
-      q.t_off = (int)roundf(toff);
-      q.rate = -2.0f * PI_F * cfo / (float)N;
-      q.scale = scale;
-      q.scaled = scaled;
-      q.pad0 = q.pad1 = 0;
-      sp = q;
-      if (a.cfo) a.cfo[f] = cfo;
-      if (a.toff) a.toff[f] = toff;
-      if (a.max_amp) a.max_amp[f] = maxv;
-    }
-    lds_barrier();
-    FSTAMP(it, 3);
-    const FrameParams q = sp;
-
-    // ---- sync symbol w on group 0 of wave w; its reads precede the first round's barrier ----
-#ifdef LORA_FUSED_NOSYNC  // profiling ablation (results invalid)
-    if (false) {
-#else
-    if (est_lane) {
-#endif
-      int64_t base;
-      int cg;
-      sym_base(wv, N, len, q.t_off, base, cg);
-      const float start = q.rate * ((float)((uint32_t)wv * (uint32_t)N) + (float)q.t_off / 1.0f);
-      cf in[P], z[P];
-      lds_points<SF>(frame, wv, (int)(base - (int64_t)wv * N), l, scale, in);
-      rotate_place<SF, true, 0>(in, z, start, q.rate, false, nullptr, l);
-      const uint64_t key = group_max(fft_key<SF, false, 0>(z, er + wv * ROW, l, b), T);
-      if (l == 0) swl[wv] = key_index(key);
-    }
-    FSTAMP(it, 4);
-
-    // ---- data symbols ----
-#ifdef LORA_FUSED_NODATA  // profiling ablation (results invalid): no data symbols
-    const int per = 0;
-#else
-    const int per = a.total - 2;
-#endif
-    const int spb = nthr / T;
-    const bool down = q.t_off < 0;
-    for (int r0 = 0; r0 < per; r0 += spb) {
-      const int k = r0 + g;
-      const bool valid = k < per;
-      const int s = 2 + (down ? per - 1 - k : k);
-      cf in[P], z[P];
-      if (valid) {
-        int64_t base;
-        int cg;
-        sym_base(s, N, len, q.t_off, base, cg);
-        const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / 1.0f);
-        lds_points<SF>(frame, s, (int)(base - (int64_t)s * N), l, scale, in);
-        rotate_place<SF, true, 0, FAST>(in, z, start, q.rate, false, nullptr, l);
-      }
-      lds_barrier();  // every read of this round precedes the in-place transposes
-      if (valid) {
-        const uint64_t key = group_max(fft_key<SF, false, 0>(z, frame + s * ROW, l, b), T);
-        if (l == 0 && a.syms) a.syms[f * a.sym_stride + (s - 2)] = (uint16_t)key_index(key);
-      }
-    }
-    FSTAMP(it, 5);
-    lds_barrier();  // the frame's LDS is reloaded next; swl complete
-    FSTAMP(it, 6);
-    if (tid == 0 && a.sync) {
-      constexpr unsigned shift = SF - 4;
-      a.sync[f] = (uint8_t)((((swl[0] >> shift) & 0x0f) << 4) | ((swl[1] >> shift) & 0x0f));
-    }
-  }
-}
-
-template <int SF, int MODE, bool FAST>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
-LORA_SCALAR_FP32 k_frame_fused(KArgs a, int nrows, int64_t frames, int stagger_ticks) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ float wmax[8];
-  __shared__ FrameParams sp;
-  __shared__ EstCand ec[2];
-  __shared__ uint32_t swl[2];
-  (void)stagger_ticks;
-  fused_frame<SF, MODE, FAST>(a, nrows, blockIdx.x, smem, wmax, sp, ec, swl, 0);
-}
-
-template <int SF, int MODE, bool FAST>
-bool launch_fused_mode(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st) {
-  using G = Geo<SF>;
-  constexpr int T = G::T;
-  const int nrows = (int)((a.frame_len + G::N - 1) / G::N);
-  const size_t lds = sizeof(cf) * (size_t)(nrows + 2) * lds_row<SF>() + FusedTables<SF>::BYTES;
-  if (lds > lds_max) return false;
-  const void* fn = (const void*)k_frame_fused<SF, MODE, FAST>;
-  if (lds > 64 * 1024)
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
-  // one round of data symbols per frame when it fits 512 threads (>= 2 waves: the
-  // estimate runs symbols 0 and 1 on waves 0 and 1)
-  const int64_t want = (int64_t)(a.total - 2) * T;
-  int block = 128;
-  while (block < 512 && block < want) block *= 2;
-  // persistent: as many workgroups as fit at once, each looping over frames
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds) != hipSuccess || per_cu < 1)
-    return false;
-  const int64_t grid = frames;
-  static const int stagger = [] {  // 100 MHz ticks (LORA_MI355X_STAGGER, default 3 us)
-    const char* e = std::getenv("LORA_MI355X_STAGGER");
-    return e ? std::atoi(e) : 300;
-  }();
-  hipLaunchKernelGGL((k_frame_fused<SF, MODE, FAST>), dim3((unsigned)grid), dim3(block), lds, st, a, nrows, frames,
-                     per_cu >= 2 ? stagger : 0);
-  return true;
-}
-
-template <int SF>
-bool launch_fused_sf(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st) {
-  if (a.fast_rot)
-    return a.dechirp ? launch_fused_mode<SF, 0, true>(a, frames, lds_max, st)
-                     : launch_fused_mode<SF, 1, true>(a, frames, lds_max, st);
-  return a.dechirp ? launch_fused_mode<SF, 0, false>(a, frames, lds_max, st)
-                   : launch_fused_mode<SF, 1, false>(a, frames, lds_max, st);
-}
-
-// ---- streaming speculative demod (SF 7-10: a symbol within one wave) -----------------
-// The speculative symbol pass as a persistent kernel that keeps the next symbol group's
-// IQ in flight while it transforms the current one.  Ablations of k_demod_fast<SPEC>
-// (tools/exp/spec_ablate.sh) put 42 % of its time on the IQ gathers: at the 4-waves/SIMD
-// ceiling its waves issue their loads and then wait, and every dechirp-table and twiddle
-// load after them waits too (vmcnt retires in order).  Here:
-//   * one workgroup of 8 waves per CU walks the symbol groups (64/T symbols = 1,024
-//     points per wave) in wave-interleaved order;
-//   * each group's windows arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
-//     instruction, no VGPR destination): 8 pieces + one dword piece for the last sample
-//     of an odd-aligned window, issued one group AHEAD into the other of two per-wave
-//     buffers, and waited for with a counted vmcnt;
-//   * nothing else in the loop is a vector-memory load: the dechirp table sits in LDS,
-//     the lane's pass twiddles and pass-1 twiddles in registers (loaded once), the frame
-//     offsets come by scalar loads, and the two result stores are counted;
-//   * a group's buffer, once read into registers, is the symbol rows of its transposes.
-// Arithmetic is k_demod_fast<SF, MODE, 0, true, true>'s, operation for operation (the
-// same dechirp, window maximum, hardware rotation with fused multiply-adds, butterflies
-// and twiddle values, margin), so margins, maxima and symbols are identical to it.
-#ifndef LORA_STREAM_ABL
-#define LORA_STREAM_ABL 0  // A/B only (results invalid): 1 = no DMA issued, 2 = no transform, 4 = no dechirp
-#endif
-// Geometry of the streaming kernel: P points per lane, T = N/P lanes per symbol, a wave
-// group of SPWV = 64/T symbols (1,024 or 512 points).  P = 16 is Geo<SF>'s shape; P = 8
-// (SF 7: 16 lanes per symbol) halves a wave's LDS so 16 waves fit a CU: pass 1 radix-2 +
-// radix-4 (stages m = 1, 2), then two radix-4 LDS passes (m = 8, 32) instead of one
-// register-blocked radix-16 pass - kissfft's butterflies, twiddles and order either way.
-template <int SF, int PP>
-struct StreamGeo {
-  static constexpr int N = 1 << SF;
-  static constexpr int P = PP;
-  static constexpr int T = N / P;
-  static constexpr int R1 = (SF & 1) ? 8 : 16;                  // pass-1 span
-  static constexpr int LOGR1 = (SF & 1) ? 3 : 4;
-  static constexpr int G1 = P / R1;
-  static constexpr bool R2FIRST = (SF & 1) != 0;
-  static constexpr int X = N / R1;
-  static constexpr int RA = X >= 16 && P >= 16 ? 16 : 4;         // pass-A span
-  static constexpr int RB = X / RA;                              // pass-B span (1 = none)
-  static constexpr int NPASS = RB > 1 ? 3 : 2;
-  static constexpr int MA_A = R1, MA_B = R1 * RA;
-  static constexpr int SPWV = 64 / T;                            // symbols per wave group
-  static constexpr int ROWC = (lds_row<SF>() + 1) & ~1;          // row stride in complex (16-B multiple)
-  static constexpr int ROWB = ROWC * 8;
-  static constexpr int PIECES = N / 128;                         // 1-KiB DMA pieces per symbol
-  static constexpr int BUFB = SPWV * ROWB;
-  static constexpr int TAILB = 256;                              // 64 lanes x 4 B (last-sample piece)
-  static constexpr int PARB = SPWV * 32;
-  static constexpr int WAVEB = 2 * (BUFB + TAILB + PARB);
-  static constexpr int WAVES = P == 8 ? 16 : 8;                  // waves per workgroup (one per CU)
-  static constexpr int NDMA = SPWV * PIECES + 1;                 // DMA instructions per group
-  static_assert(G1 >= 1 && RB <= 16 && (RB == 1 || RB == 4 || RB == 16) && RA * RB * R1 == N, "pass shape");
-  static_assert(P == 16 || (P == 8 && SF == 7), "P = 8 only for SF 7");
-  static_assert(ROWC >= N + 1, "a row holds the window plus the odd-alignment shift");
-};
-
-// Pass-1 register of point q: (q % G1) * R1 + leaf_pos(R1, q / G1), folded at compile time.
-template <int P, int G1, int R1>
-struct ZIdx {
-  int v[P];
-};
-template <int P, int G1, int R1>
-constexpr ZIdx<P, G1, R1> make_zidx() {
-  ZIdx<P, G1, R1> z{};
-  for (int q = 0; q < P; ++q) z.v[q] = (q % G1) * R1 + leaf_pos(R1, q / G1);
-  return z;
-}
-
-// group_reduce2 for groups of T <= 64 lanes (wave-local)
-template <int T>
-__device__ __forceinline__ void group_reduce2_w(float& a, float& b) {
-#pragma unroll
-  for (int o = T >> 1; o > 0; o >>= 1) {
-    a = fmaxf(a, __shfl_xor(a, o, 64));
-    b = fmaxf(b, __shfl_xor(b, o, 64));
-  }
-}
-
-struct StreamSym {  // one symbol of a group (LDS, written when its DMA is issued)
-  float start, rate;
-  int cg, shift;
-  int64_t marg_idx, sym_idx;
-};
-
-__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)p; }
-
-// LDS-DMA: each lane's 16 (4) bytes at g land at LDS byte lds + lane*16 (lane*4).  M0 is
-// written and restored inside the statement (cdna_hip_programming.md, LDS-DMA recipe);
-// hipcc does not count these loads, the kernel waits for them itself.
-__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-}
-__device__ __forceinline__ void dma16(const void* g, uint32_t lds) {
-  unsigned keep;
-  lds = __builtin_amdgcn_readfirstlane(lds);
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds)
-               : "memory");
-}
-__device__ __forceinline__ void dma4(const void* g, uint32_t lds) {
-  unsigned keep;
-  lds = __builtin_amdgcn_readfirstlane(lds);
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds)
-               : "memory");
-}
-// Frame offsets by scalar loads (wave-uniform frame): rate (+8) and t_off (+16).
-__device__ __forceinline__ void sload_fp(const FrameParams* p, float& rate, int& t_off) {
-  uint32_t r, t;
-  p = reinterpret_cast<const FrameParams*>(rfl64(reinterpret_cast<uint64_t>(p)));
-  asm volatile("s_load_dword %0, %2, 0x8\n\ts_load_dword %1, %2, 0x10\n\ts_waitcnt lgkmcnt(0)"
-               : "=&s"(r), "=&s"(t)
-               : "s"(p)
-               : "memory");
-  rate = __uint_as_float(r);
-  t_off = (int)t;
-}
-__device__ __forceinline__ void store_u16(uint16_t* p, uint32_t v) {
-  asm volatile("global_store_short %0, %1, off" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void store_f2(float2* p, float2 v) {
-  asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-}
-
-// Issue group g's windows into buffer `buf` (wave-uniform LDS byte address) and record
-// each symbol's parameters in `par`.  Symbols past `work` mirror the last one (identical
-// values to identical addresses).  All control flow is wave-uniform.
-template <int SF, int PP>
-__device__ __forceinline__ void stream_issue(const KArgs& a, int g, int work, int per, uint32_t buf,
-                                             uint32_t tail, StreamSym* par, int lane) {
-  using SG = StreamGeo<SF, PP>;
-  constexpr int N = SG::N, SPWV = SG::SPWV;
-  const int w0 = g * SPWV;
-  int wc = w0 < work ? w0 : work - 1;
-  int f = wc / per, r = wc - f * per;
-  const char* tsrc = nullptr;
-#pragma unroll
-  for (int j = 0; j < SPWV; ++j) {
-    if (j > 0 && w0 + j < work) {
-      ++wc;
-      if (++r == per) {
-        r = 0;
-        ++f;
-      }
-    }
-    float rate;
-    int t_off;
-    sload_fp(a.fp_spec + f, rate, t_off);
-    const int s = 2 + r;
-    int64_t base;
-    int cg;
-    sym_base(s, N, a.frame_len, t_off, base, cg);
-    const char* B = reinterpret_cast<const char*>(a.iq + (int64_t)f * a.frame_stride + base);
-    const int shift = (int)(((uintptr_t)B >> 3) & 1);
-    const char* A = B - 8 * shift;  // 16-B aligned (frames start 16-B aligned)
-#pragma unroll
-    for (int c = 0; c < SG::PIECES; ++c)
-      if (!(LORA_STREAM_ABL & 1)) dma16(A + c * 1024 + lane * 16, buf + j * SG::ROWB + c * 1024);
-    if (((lane >> 1) % SPWV) == j) tsrc = B + 8 * (N - 1) + 4 * (lane & 1);
-    if (lane == 0) {
-      StreamSym sp;
-      sp.start = rate * ((float)((uint32_t)s * (uint32_t)N) + (float)t_off);  // osr 1
-      sp.rate = rate;
-      sp.cg = cg;
-      sp.shift = shift;
-      sp.marg_idx = wc;
-      sp.sym_idx = (int64_t)f * a.sym_stride + r;
-      par[j] = sp;
-    }
-  }
-  if (!(LORA_STREAM_ABL & 1)) dma4(tsrc, tail);
-}
-
-// pass_lds with the lane's twiddles in registers: w[gg * (R == 16 ? 15 : 3) + j] =
-// twT[j * MA + k] of group gg (lora::twT_index), same butterflies and order.
-template <int R, int MA, int SF, int T, int P, bool LAST>
-__device__ __forceinline__ void pass_lds_rw(cf* row, cf* x, int l, const cf* w, uint64_t& key, float* second) {
-  constexpr int NG = P / R, NT = R == 16 ? 15 : 3;
-#pragma unroll
-  for (int gg = 0; gg < NG; ++gg) {
-    const int GI = l + T * gg;
-    const int k = GI % MA, cc = GI / MA;
-    cf* xs = x + gg * R;
-    const cf* rb = row + lds_slot<SF>(cc * MA * R + k);
-#pragma unroll
-    for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
-    const cf* wg = w + gg * NT;
-#pragma unroll
-    for (int blk = 0; blk < R; blk += 4) bfly4<true>(xs[blk], xs[blk + 1], xs[blk + 2], xs[blk + 3], wg[0], wg[1], wg[2]);
-    if constexpr (R == 16) {
-#pragma unroll
-      for (int uu = 0; uu < 4; ++uu)
-        bfly4<true>(xs[uu], xs[uu + 4], xs[uu + 8], xs[uu + 12], wg[3 + 3 * uu], wg[4 + 3 * uu], wg[5 + 3 * uu]);
-    }
-  }
-  if constexpr (LAST) {
-    float best = 0.0f, sec = 0.0f;
-    uint32_t bi = (uint32_t)l;
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-#pragma unroll
-      for (int gg = 0; gg < NG; ++gg) {
-        const cf v = x[gg * R + u];
-        const float m2 = v.re * v.re + v.im * v.im;
-        const uint32_t bin = (uint32_t)(l + T * gg + MA * u);
-        sec = __builtin_amdgcn_fmed3f(sec, m2, best);
-        if (m2 > best) {
-          best = m2;
-          bi = bin;
-        }
-      }
-    key = ((uint64_t)__float_as_uint(best) << 32) | (uint32_t)(~bi);
-    *second = sec;
-  }
-}
-
-// pass_regs<R, R2, N, 1, UNIT = true, FMA = true>(x, 0, tw) with tw[m * N / R] = t1[m].
-template <int R, bool R2>
-__device__ __forceinline__ void pass1_rw(cf* x, const cf* t1) {
-  int S = 1;
-  if constexpr (R2) {
-#pragma unroll
-    for (int b = 0; b < R; b += 2) bfly2_unit(x[b], x[b + 1]);
-    S = 2;
-  }
-#pragma unroll
-  for (; S < R; S *= 4) {
-    const int ms = R / (4 * S);  // tw index q*uu*fs, fs = N/(4S) = ms * (N/R)
-#pragma unroll
-    for (int blk = 0; blk < R; blk += 4 * S) {
-#pragma unroll
-      for (int uu = 0; uu < S; ++uu) {
-        if (uu == 0)
-          bfly4_unit(x[blk], x[blk + S], x[blk + 2 * S], x[blk + 3 * S]);
-        else
-          bfly4<true>(x[blk + uu], x[blk + uu + S], x[blk + uu + 2 * S], x[blk + uu + 3 * S], t1[uu * ms],
-                      t1[2 * uu * ms], t1[3 * uu * ms]);
-      }
-    }
-  }
-}
-
-template <int SF, int MODE, int PP>
-__global__ void __launch_bounds__((StreamGeo<SF, PP>::WAVES * 64))
-__attribute__((amdgpu_waves_per_eu(StreamGeo<SF, PP>::WAVES / 4)))
-LORA_SCALAR_FP32 k_demod_stream(KArgs a, int work, int ngroups) {
-  using SG = StreamGeo<SF, PP>;
-  constexpr int N = SG::N, T = SG::T, P = SG::P, R1 = SG::R1, SPWV = SG::SPWV, NT = SG::WAVES * 64;
-  constexpr int NGA = P / SG::RA, NGB = SG::NPASS == 3 ? P / SG::RB : 0;
-  constexpr int NTA = SG::RA == 16 ? 15 : 3, NTB = SG::RB == 16 ? 15 : 3;
-  constexpr int TABB = MODE == 0 ? 2 * N * 8 : 0;
-  constexpr ZIdx<P, SG::G1, R1> ZI = make_zidx<P, SG::G1, R1>();
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  cf* dtab = reinterpret_cast<cf*>(smem);
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int per = a.total - 2;
-
-  // ---- prologue: dechirp table to LDS, the lane's twiddles and digit-reverse rows ----
-  if constexpr (MODE == 0)
-    for (int i = tid; i < 2 * N; i += NT) dtab[i] = a.down[i];
-  const int l = lane % T, j = lane / T;
-  cf t1[12];
-#pragma unroll
-  for (int m = 0; m < 12; ++m) t1[m] = (m * (N / R1) < N) ? a.tw[m * (N / R1)] : cf{0.0f, 0.0f};
-  // the lane's pass twiddles, read from the natural table at the slot-major copy's
-  // indices (lora::twT_index; the copy, when the plan has one, holds the same values)
-  cf twA[NGA * NTA];
-#pragma unroll
-  for (int gg = 0; gg < NGA; ++gg)
-#pragma unroll
-    for (int jj = 0; jj < NTA; ++jj) twA[gg * NTA + jj] = a.tw[twT_index(N, SG::MA_A, jj, (l + T * gg) % SG::MA_A)];
-  cf twB[NGB > 0 ? NGB * NTB : 1];
-  if constexpr (NGB > 0) {
-#pragma unroll
-    for (int gg = 0; gg < NGB; ++gg)
-#pragma unroll
-      for (int jj = 0; jj < NTB; ++jj) twB[gg * NTB + jj] = a.tw[twT_index(N, SG::MA_B, jj, (l + T * gg) % SG::MA_B)];
-  }
-  int c[SG::G1];
-#pragma unroll
-  for (int h = 0; h < SG::G1; ++h) c[h] = (int)(a.rev[l + T * h] >> SG::LOGR1);
-  // settle every prologue load here: no compiler-counted vector load may remain pending
-  // inside the loop (its wait would also drain the DMA in flight)
-#pragma unroll
-  for (int m = 0; m < 12; ++m) asm volatile("" : "+v"(t1[m].re), "+v"(t1[m].im));
-#pragma unroll
-  for (int m = 0; m < NGA * NTA; ++m) asm volatile("" : "+v"(twA[m].re), "+v"(twA[m].im));
-  if constexpr (NGB > 0) {
-#pragma unroll
-    for (int m = 0; m < NGB * NTB; ++m) asm volatile("" : "+v"(twB[m].re), "+v"(twB[m].im));
-  }
-#pragma unroll
-  for (int h = 0; h < SG::G1; ++h) asm volatile("" : "+v"(c[h]));
-  __syncthreads();
-
-  unsigned char* wbase = smem + TABB + wave * SG::WAVEB;
-  auto bufp = [&](int b) { return wbase + b * SG::BUFB; };
-  auto tailp = [&](int b) { return wbase + 2 * SG::BUFB + b * SG::TAILB; };
-  auto parp = [&](int b) { return reinterpret_cast<StreamSym*>(wbase + 2 * (SG::BUFB + SG::TAILB) + b * SG::PARB); };
-
-  const int NW = gridDim.x * SG::WAVES;
-  int g = blockIdx.x * SG::WAVES + wave;
-  if (g < ngroups) stream_issue<SF, PP>(a, g, work, per, lds_u32(bufp(0)), lds_u32(tailp(0)), parp(0), lane);
-  for (int it = 0; g < ngroups; ++it, g += NW) {
-    const int nb = it & 1;
-    const bool more = g + NW < ngroups;
-    if (more) stream_issue<SF, PP>(a, g + NW, work, per, lds_u32(bufp(nb ^ 1)), lds_u32(tailp(nb ^ 1)), parp(nb ^ 1), lane);
-    // group g's pieces landed: younger are the previous group's 2 stores (it > 0) and the
-    // next group's NDMA pieces (more); vmcnt retires in issue order
-    if (it > 0) {
-      if (more)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SG::NDMA + 2) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      if (more)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SG::NDMA) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const StreamSym sp = parp(nb)[j];
-    cf* row = reinterpret_cast<cf*>(bufp(nb) + j * SG::ROWB);
-    const cf* src = row + sp.shift + l;
-    cf in[P], z[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) in[q] = src[T * q];
-    {  // the window's last sample of an odd-aligned window came in the dword piece
-      const cf tv = reinterpret_cast<const cf*>(tailp(nb))[j];
-      if (l == T - 1 && sp.shift) in[P - 1] = tv;
-    }
-    wave_sync();  // every lane's samples are in registers before the row is reused
-    if constexpr (LORA_STREAM_ABL & 2) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int q = 0; q < P; ++q) acc = amax3(acc, in[q]);
-      store_u16(a.syms + sp.sym_idx, __float_as_uint(acc) & 0xFFFFu);
-      store_f2(reinterpret_cast<float2*>(a.spec_marg) + sp.marg_idx, make_float2(acc, acc));
-      continue;
-    }
-    if constexpr (MODE == 0 && !(LORA_STREAM_ABL & 4)) {
-      const cf* dl = dtab + sp.cg + l;
-#pragma unroll
-      for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[T * q]);
-    }
-    float pm = 0.0f;
-#pragma unroll
-    for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
-    {
-      constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        const float ph = sp.start + sp.rate * (float)(l + T * q);
-        const float rev = __builtin_amdgcn_fractf(ph * INV_2PI);
-        z[ZI.v[q]] =
-            cmul_t<true>(in[q], cf{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)});
-      }
-    }
-    asm volatile("" : "+v"(pm));
-#pragma unroll
-    for (int h = 0; h < SG::G1; ++h) pass1_rw<R1, SG::R2FIRST>(z + h * R1, t1);
-#pragma unroll
-    for (int h = 0; h < SG::G1; ++h)
-#pragma unroll
-      for (int u = 0; u < R1; ++u) row[lds_slot<SF>(c[h] * R1) + u] = z[h * R1 + u];
-    wave_sync();
-    uint64_t lkey = 0;
-    float sec = 0.0f;
-    if constexpr (SG::NPASS == 2) {
-      pass_lds_rw<SG::RA, SG::MA_A, SF, T, P, true>(row, z, l, twA, lkey, &sec);
-    } else {
-      pass_lds_rw<SG::RA, SG::MA_A, SF, T, P, false>(row, z, l, twA, lkey, &sec);
-      wave_sync();
-      write_pass<SG::RA, SG::MA_A, SF, T, P>(row, z, l);
-      wave_sync();
-      pass_lds_rw<SG::RB, SG::MA_B, SF, T, P, true>(row, z, l, twB, lkey, &sec);
-    }
-    const uint64_t key = group_max(lkey, T);
-    float r2 = lkey == key ? sec : key_value(lkey);
-    group_reduce2_w<T>(r2, pm);
-    // every lane of the symbol stores the symbol's (identical) results: 2 full-wave stores
-    store_u16(a.syms + sp.sym_idx, key_index(key) & 0xFFFFu);
-    store_f2(reinterpret_cast<float2*>(a.spec_marg) + sp.marg_idx, make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm));
-  }
-}
-
-template <int SF, int MODE, int PP>
-bool launch_stream(const KArgs& a, int64_t work, hipStream_t st) {
-  using SG = StreamGeo<SF, PP>;
-  constexpr int TABB = MODE == 0 ? 2 * (1 << SF) * 8 : 0;
-  const size_t lds = TABB + SG::WAVES * SG::WAVEB;
-  static_assert(TABB + SG::WAVES * SG::WAVEB <= 160 * 1024, "LDS budget");
-  if (work <= 0 || work >= (int64_t(1) << 31) || !a.syms || !a.spec_marg || !a.fp_spec || !a.tw || !a.rev ||
-      (MODE == 0 && !a.down) || a.total < 3)
-    return false;
-  // frames start 16-byte aligned, so a window's 16-B aligned superset stays in its frame
-  if ((a.frame_stride & 1) || (reinterpret_cast<uintptr_t>(a.iq) & 15)) return false;
-  static int ncu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  if (hipFuncSetAttribute((const void*)k_demod_stream<SF, MODE, PP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
-    return false;
-  const int ngroups = (int)((work + SG::SPWV - 1) / SG::SPWV);
-  const int grid = std::max(1, std::min(ncu, (ngroups + SG::WAVES - 1) / SG::WAVES));
-  hipLaunchKernelGGL((k_demod_stream<SF, MODE, PP>), dim3((unsigned)grid), dim3(SG::WAVES * 64), lds, st, a, (int)work,
-                     ngroups);
-  return true;
-}
-
-// ---- register-prefetch speculative demod (SF 7) ---------------------------------------
-// The streaming kernel's alternative without LDS-DMA: persistent 4-wave workgroups at
-// 4 waves/SIMD, P = 8 points per lane (StreamGeo<7, 8>: 16 lanes per symbol, 4 symbols
-// per wave group), and the next group's samples loaded into registers (8 x 8 B per lane)
-// before the current group is transformed.  No other vector-memory load is in the loop
-// (dechirp table: registers for the common phase 0, else LDS; twiddles: registers), so
-// hipcc's own vmcnt bookkeeping waits for exactly the prefetch when its values are used.
-// Same arithmetic as k_demod_fast<7, MODE, 0, true, true>.
-#ifndef LORA_PF_DREG
-#define LORA_PF_DREG 1  // keep the phase-0 dechirp values of the lane in registers
-#endif
-struct PfSym {
-  const cf* x;  // the lane's first sample of its window
-  float start, rate;
-  int cg, marg_idx;
-  int64_t sym_idx;
-};
-
-template <int SF>
-__device__ __forceinline__ PfSym pf_params(const KArgs& a, int g, int work, int per, int lane) {
-  using SG = StreamGeo<SF, 8>;
-  constexpr int N = SG::N, T = SG::T, SPWV = SG::SPWV;
-  const int w0 = g * SPWV;
-  int wc = w0 < work ? w0 : work - 1;
-  int f = wc / per, r = wc - f * per;
-  PfSym me{};
-  const int jl = lane / T, l = lane % T;
-#pragma unroll
-  for (int j = 0; j < SPWV; ++j) {
-    if (j > 0 && w0 + j < work) {
-      ++wc;
-      if (++r == per) {
-        r = 0;
-        ++f;
-      }
-    }
-    float rate;
-    int t_off;
-    sload_fp(a.fp_spec + f, rate, t_off);
-    const int s = 2 + r;
-    int64_t base;
-    int cg;
-    sym_base(s, N, a.frame_len, t_off, base, cg);
-    if (jl == j) {
-      me.x = a.iq + (int64_t)f * a.frame_stride + base + l;
-      me.start = rate * ((float)((uint32_t)s * (uint32_t)N) + (float)t_off);  // osr 1
-      me.rate = rate;
-      me.cg = cg;
-      me.marg_idx = wc;
-      me.sym_idx = (int64_t)f * a.sym_stride + r;
-    }
-  }
-  return me;
-}
-
-template <int SF, int MODE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-LORA_SCALAR_FP32 k_demod_pf(KArgs a, int work, int ngroups) {
-  using SG = StreamGeo<SF, 8>;
-  constexpr int N = SG::N, T = SG::T, P = SG::P, R1 = SG::R1;
-  constexpr int NGA = P / SG::RA, NGB = SG::NPASS == 3 ? P / SG::RB : 0;
-  constexpr int NTA = SG::RA == 16 ? 15 : 3, NTB = SG::RB == 16 ? 15 : 3;
-  constexpr int TABB = MODE == 0 ? 2 * N * 8 : 0;
-  constexpr ZIdx<P, SG::G1, R1> ZI = make_zidx<P, SG::G1, R1>();
-  static_assert(SG::NPASS == 3, "two LDS passes");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  cf* dtab = reinterpret_cast<cf*>(smem);
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int per = a.total - 2;
-  const int l = lane % T, j = lane / T;
-
-  if constexpr (MODE == 0)
-    for (int i = tid; i < 2 * N; i += 256) dtab[i] = a.down[i];
-  cf t1[12];
-#pragma unroll
-  for (int m = 0; m < 12; ++m) t1[m] = (m * (N / R1) < N) ? a.tw[m * (N / R1)] : cf{0.0f, 0.0f};
-  cf twA[NGA * NTA], twB[NGB * NTB];
-#pragma unroll
-  for (int gg = 0; gg < NGA; ++gg)
-#pragma unroll
-    for (int jj = 0; jj < NTA; ++jj) twA[gg * NTA + jj] = a.tw[twT_index(N, SG::MA_A, jj, (l + T * gg) % SG::MA_A)];
-#pragma unroll
-  for (int gg = 0; gg < NGB; ++gg)
-#pragma unroll
-    for (int jj = 0; jj < NTB; ++jj) twB[gg * NTB + jj] = a.tw[twT_index(N, SG::MA_B, jj, (l + T * gg) % SG::MA_B)];
-  int c0 = (int)(a.rev[l] >> SG::LOGR1);
-  cf dreg[P];
-#pragma unroll
-  for (int q = 0; q < P; ++q) dreg[q] = (MODE == 0 && LORA_PF_DREG) ? a.down[l + T * q] : cf{0.0f, 0.0f};
-  // settle every prologue load here (a load still pending at the loop would be waited
-  // for inside it, behind the prefetch)
-#pragma unroll
-  for (int m = 0; m < 12; ++m) asm volatile("" : "+v"(t1[m].re), "+v"(t1[m].im));
-#pragma unroll
-  for (int m = 0; m < NGA * NTA; ++m) asm volatile("" : "+v"(twA[m].re), "+v"(twA[m].im));
-#pragma unroll
-  for (int m = 0; m < NGB * NTB; ++m) asm volatile("" : "+v"(twB[m].re), "+v"(twB[m].im));
-#pragma unroll
-  for (int q = 0; q < P; ++q) asm volatile("" : "+v"(dreg[q].re), "+v"(dreg[q].im));
-  asm volatile("" : "+v"(c0));
-  __syncthreads();
-
-  const int NW = gridDim.x * 4;
-  int g = blockIdx.x * 4 + wave;
-  if (g >= ngroups) return;
-  cf* row = reinterpret_cast<cf*>(smem + TABB + (wave * SG::SPWV + j) * SG::ROWB);
-  PfSym nxt = pf_params<SF>(a, g, work, per, lane);
-  cf nin[P];
-#pragma unroll
-  for (int q = 0; q < P; ++q) nin[q] = nxt.x[T * q];
-  for (;;) {
-    const PfSym cur = nxt;
-    cf in[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) in[q] = nin[q];
-    // the next group's samples (the last iteration re-reads its own windows, from L2)
-    const int gn = g + NW;
-    const bool more = gn < ngroups;
-    nxt = pf_params<SF>(a, more ? gn : g, work, per, lane);
-#pragma unroll
-    for (int q = 0; q < P; ++q) nin[q] = nxt.x[T * q];
-    if constexpr (MODE == 0) {
-      if (LORA_PF_DREG && __all(cur.cg == 0)) {
-#pragma unroll
-        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dreg[q]);
-      } else {
-        const cf* dl = dtab + cur.cg + l;
-#pragma unroll
-        for (int q = 0; q < P; ++q) in[q] = cmul(in[q], dl[T * q]);
-      }
-    }
-    float pm = 0.0f;
-#pragma unroll
-    for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
-    cf z[P];
-    {
-      constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        const float ph = cur.start + cur.rate * (float)(l + T * q);
-        const float rev = __builtin_amdgcn_fractf(ph * INV_2PI);
-        z[ZI.v[q]] = cmul_t<true>(in[q], cf{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)});
-      }
-    }
-    asm volatile("" : "+v"(pm));
-    pass1_rw<R1, SG::R2FIRST>(z, t1);
-#pragma unroll
-    for (int u = 0; u < R1; ++u) row[lds_slot<SF>(c0 * R1) + u] = z[u];
-    wave_sync();
-    uint64_t lkey = 0;
-    float sec = 0.0f;
-    pass_lds_rw<SG::RA, SG::MA_A, SF, T, P, false>(row, z, l, twA, lkey, &sec);
-    wave_sync();
-    write_pass<SG::RA, SG::MA_A, SF, T, P>(row, z, l);
-    wave_sync();
-    pass_lds_rw<SG::RB, SG::MA_B, SF, T, P, true>(row, z, l, twB, lkey, &sec);
-    const uint64_t key = group_max(lkey, T);
-    float r2 = lkey == key ? sec : key_value(lkey);
-    group_reduce2_w<T>(r2, pm);
-    if (l == 0) {
-      a.syms[cur.sym_idx] = (uint16_t)key_index(key);
-      reinterpret_cast<float2*>(a.spec_marg)[cur.marg_idx] = make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm);
-    }
-    wave_sync();  // the row's last reads before the next group's write-back
-    if (!more) break;
-    g = gn;
-  }
-}
-
-template <int SF, int MODE>
-bool launch_pf(const KArgs& a, int64_t work, hipStream_t st) {
-  using SG = StreamGeo<SF, 8>;
-  constexpr int TABB = MODE == 0 ? 2 * (1 << SF) * 8 : 0;
-  const size_t lds = TABB + 4 * SG::SPWV * SG::ROWB;
-  if (work <= 0 || work >= (int64_t(1) << 31) || !a.syms || !a.spec_marg || !a.fp_spec || !a.tw || !a.rev ||
-      (MODE == 0 && !a.down) || a.total < 3)
-    return false;
-  static int ncu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  static int per_cu = [] {
-    const char* e = std::getenv("LORA_MI355X_PF_WG");  // A/B knob: workgroups per CU
-    return e ? std::max(1, std::atoi(e)) : 4;
-  }();
-  const int ngroups = (int)((work + SG::SPWV - 1) / SG::SPWV);
-  const int grid = std::max(1, std::min(ncu * per_cu, (ngroups + 3) / 4));
-  hipLaunchKernelGGL((k_demod_pf<SF, MODE>), dim3((unsigned)grid), dim3(256), lds, st, a, (int)work, ngroups);
-  return true;
 }
 
 template <int SF>
@@ -2216,19 +1195,19 @@ bool launch_est_sf(const KArgs& a, int64_t frames, hipStream_t st) {
   return launch_est_mode<SF, 2>(a, frames, st);
 }
 
-template <int SF, int MODE, int ABL = 0, bool FAST = false, bool SPEC = false>
+template <int SF, int MODE, bool FAST = false, bool SPEC = false>
 bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
   const size_t lds = G::NPASS == 1 ? 16 : sizeof(cf) * ((size_t)G::SPW * rowc + demod_twl_entries<SF, SPEC>());
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_demod_fast<SF, MODE, ABL, FAST, SPEC>,
+    if (hipFuncSetAttribute((const void*)k_demod_fast<SF, MODE, FAST, SPEC>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return false;
   const int64_t grid = (work + G::SPW - 1) / G::SPW;
-  hipLaunchKernelGGL((k_demod_fast<SF, MODE, ABL, FAST, SPEC>), dim3((unsigned)grid), dim3(256), lds, st, a, s0,
-                     work, rowc);
+  hipLaunchKernelGGL((k_demod_fast<SF, MODE, FAST, SPEC>), dim3((unsigned)grid), dim3(256), lds, st, a, s0, work,
+                     rowc);
   return true;
 }
 
@@ -2240,33 +1219,8 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   } else {
     const int64_t work = frames * (int64_t)(a.total - 2);
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
-    if (stage == 1) {
-      if constexpr (SF >= 7 && SF <= 10) {
-        // LORA_MI355X_STREAM (A/B, opt-in): "1" = SF 7 (P = 8), "all" = SF 7-10, unset/"0" = off
-        static const int stream = [] {
-          const char* e = std::getenv("LORA_MI355X_STREAM");
-          return !e ? 0 : e[0] == '0' ? 0 : (e[0] == 'a' ? 2 : 1);
-        }();
-        constexpr int PP = SF == 7 ? 8 : 16;
-        if constexpr (SF == 7) {
-          static const bool pf = [] {
-            const char* e = std::getenv("LORA_MI355X_PF");
-            return e && e[0] == '1';
-          }();
-          if (pf && (a.fast_rot || a.spec_hw) &&
-              (a.dechirp ? launch_pf<SF, 0>(a, work, st) : launch_pf<SF, 1>(a, work, st)))
-            return true;
-        }
-        if (stream && (SF == 7 || stream == 2) && (a.fast_rot || a.spec_hw) &&
-            (a.dechirp ? launch_stream<SF, 0, PP>(a, work, st) : launch_stream<SF, 1, PP>(a, work, st)))
-          return true;
-      }
-      if (a.fast_rot || a.spec_hw)
-        return a.dechirp ? launch_mode<SF, 0, 0, true, true>(a, 2, work, st)
-                         : launch_mode<SF, 1, 0, true, true>(a, 2, work, st);
-      return a.dechirp ? launch_mode<SF, 0, 0, false, true>(a, 2, work, st)
-                       : launch_mode<SF, 1, 0, false, true>(a, 2, work, st);
-    }
+    if (stage == 1)
+      return a.dechirp ? launch_mode<SF, 0, true, true>(a, 2, work, st) : launch_mode<SF, 1, true, true>(a, 2, work, st);
     return a.dechirp ? launch_est_mode<SF, 0, 2>(a, frames, st) : launch_est_mode<SF, 1, 2>(a, frames, st);
   }
 }
@@ -2274,27 +1228,11 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
 template <int SF>
 bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   const bool simple = a.mode == LORA_MODE_LEGACY && a.osr == 1 && !a.hann;
-  if constexpr (SF == 7 || SF == 12) {
-    if (simple && a.dechirp && a.ablate) {
-      switch (a.ablate) {
-        case 1: return launch_mode<SF, 0, 1>(a, s0, work, st);
-        case 2: return launch_mode<SF, 0, 2>(a, s0, work, st);
-        case 3: return launch_mode<SF, 0, 3>(a, s0, work, st);
-        case 4: return launch_mode<SF, 0, 4>(a, s0, work, st);
-        case 5: return launch_mode<SF, 0, 5>(a, s0, work, st);
-        case 7: return launch_mode<SF, 0, 7>(a, s0, work, st);
-        case 8: return launch_mode<SF, 0, 8>(a, s0, work, st);
-        case 9: return launch_mode<SF, 0, 9>(a, s0, work, st);
-        case 12: return launch_mode<SF, 0, 12>(a, s0, work, st);
-        default: break;
-      }
-    }
-  }
   if (a.mode == LORA_MODE_RAW) return launch_mode<SF, 3>(a, s0, work, st);
   if (a.fast_rot) {  // LORA_PRECISION_FAST (include/lora_mi355x.h)
-    if (simple && a.dechirp) return launch_mode<SF, 0, 0, true>(a, s0, work, st);
-    if (simple) return launch_mode<SF, 1, 0, true>(a, s0, work, st);
-    return launch_mode<SF, 2, 0, true>(a, s0, work, st);
+    if (simple && a.dechirp) return launch_mode<SF, 0, true>(a, s0, work, st);
+    if (simple) return launch_mode<SF, 1, true>(a, s0, work, st);
+    return launch_mode<SF, 2, true>(a, s0, work, st);
   }
   if (simple && a.dechirp) return launch_mode<SF, 0>(a, s0, work, st);
   if (simple) return launch_mode<SF, 1>(a, s0, work, st);
@@ -2302,29 +1240,6 @@ bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
 }
 
 }  // namespace
-
-#ifdef LORA_FUSED_TIMING
-extern "C" int lora_debug_fused_timing(unsigned long long* host, size_t n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fused_dbg), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -5;
-}
-extern "C" int lora_debug_fused_timing_clear(void) {
-  static unsigned long long zeros[2048 * 16 * 8];
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_fused_dbg), zeros, sizeof(zeros)) == hipSuccess ? 0 : -5;
-}
-#endif
-
-bool launch_fused(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st) {
-  const bool simple = a.mode == LORA_MODE_LEGACY && a.osr == 1 && !a.hann && a.have_sync && a.total >= 2;
-  if (!simple || a.est_only || a.ablate || frames <= 0 || frames >= (int64_t(1) << 31)) return false;
-  // 16-byte loads: every frame starts 16-byte aligned
-  if ((a.frame_stride & 1) || (reinterpret_cast<uintptr_t>(a.iq) & 15)) return false;
-  switch (a.sf) {
-    case 6: return launch_fused_sf<6>(a, frames, lds_max, st);
-    case 7: return launch_fused_sf<7>(a, frames, lds_max, st);
-    case 8: return launch_fused_sf<8>(a, frames, lds_max, st);
-    default: return false;
-  }
-}
 
 bool launch_spec(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   switch (a.sf) {

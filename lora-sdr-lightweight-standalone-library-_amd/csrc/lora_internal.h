@@ -30,7 +30,6 @@ struct KArgs {
   float* toff;
   float* max_amp;
   int est_only;  // lora_estimate_offsets_batch: all symbols, raw samples, outputs only
-  int ablate;    // profiling-only ablation mask (LORA_MI355X_ABLATE), 0 in production
   int fast_rot;  // LORA_PRECISION_FAST: hardware sin/cos rotation in the symbol demod
   const cf* twTA;  // fast kernels: slot-major twiddles of LDS pass A / B (or null)
   const cf* twTB;
@@ -47,8 +46,6 @@ struct KArgs {
   float* spec_marg = nullptr;      // [frame][data symbol][2]: |X1| - |X2|, window max(|I|,|Q|)
   uint32_t* spec_max = nullptr;    // writable alias of maxbits: [frame] max outside the windows
   unsigned int* spec_fix = nullptr;
-  int spec_hw = 0;  // the speculative demod rotates with the hardware sine/cosine; every
-                    // frame's symbols are certified against the exact reference
 };
 
 // Shape of the fast kernels' LDS passes for SF >= 6 (lora_demod_fast.hip Geo<SF>): pass-1
@@ -89,11 +86,6 @@ void host_gen_chirp(std::complex<float>* out, int N, int osr, int NN, float f0, 
 // Fast symbol demodulator (lora_demod_fast.hip): register-blocked kissfft-exact FFT.
 // Returns false if the configuration is not covered (caller uses the generic kernel).
 bool launch_demod_fast(const KArgs& a, int s0, int64_t work, hipStream_t st);
-
-// Frame-resident single-read pipeline (max + estimate + every symbol in one launch, the
-// frame staged in LDS) for LEGACY osr-1 unwindowed frames of SF 6-8 whose LDS image is at
-// most lds_max bytes; false = not covered (caller runs the three-launch path).
-bool launch_fused(const KArgs& a, int64_t frames, size_t lds_max, hipStream_t st);
 
 // Speculative single-read pipeline, SF 6-12, LEGACY osr-1 unwindowed frames with >= 3
 // symbols (lora_capi.hip): stage 0 = k_est_fast<SPEC=1> (estimate on unscaled samples +

@@ -26,8 +26,7 @@ LORA_MODE_API = 1
 LORA_MODE_RAW = 2
 
 # lora_demod_last_kernels bits
-KERNEL_BITS = {"frame_max": 1, "estimate": 2, "demod": 4, "fused": 8, "generic": 16, "frame_max_wave": 32,
-               "spec": 64}
+KERNEL_BITS = {"frame_max": 1, "estimate": 2, "demod": 4, "generic": 16, "frame_max_wave": 32, "spec": 64}
 
 # Every symbol include/lora_mi355x.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED_SYMBOLS = (

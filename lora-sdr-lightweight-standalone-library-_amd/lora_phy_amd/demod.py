@@ -118,7 +118,7 @@ class DemodPlan:
     def last_kernels(self) -> set:
         """Kernels the last run() launched: {"spec", "estimate", "demod"} for the speculative
         single-read pipeline, {"frame_max", "estimate", "demod"} for the three-launch path
-        (+"generic", "frame_max_wave"), {"fused"} for the opt-in frame-resident kernel."""
+        (+"generic", "frame_max_wave")."""
         m = self._lib.lora_demod_last_kernels(self._h)
         return {k for k, b in _capi.KERNEL_BITS.items() if m & b}
 

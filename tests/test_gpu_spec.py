@@ -44,22 +44,17 @@ def bits(x):
     return np.asarray(x, np.float32).view(np.uint32)
 
 
-def check(O, amd, iq, sf, spec=True, hw=True):
+def check(O, amd, iq, sf, spec=True):
     """Run `iq` ([F, L] dechirped frames) through a fresh plan and compare every output
-    with the oracle; returns (plan, recomputed symbols).  spec=False: three-launch path;
-    hw=False: the speculative demod rotates with glibc sincosf instead of the hardware
-    sine/cosine (LORA_MI355X_SPEC_HW=0)."""
+    with the oracle; returns (plan, recomputed symbols).  spec=False: three-launch path."""
     import os
 
     if not spec:
         os.environ["LORA_MI355X_SPEC"] = "0"
-    if not hw:
-        os.environ["LORA_MI355X_SPEC_HW"] = "0"
     try:
         plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=False)
     finally:
         os.environ.pop("LORA_MI355X_SPEC", None)
-        os.environ.pop("LORA_MI355X_SPEC_HW", None)
     res = plan.run(torch.from_numpy(np.ascontiguousarray(iq)).cuda())
     torch.cuda.synchronize()
     syms = res.symbols.cpu().numpy()
@@ -95,36 +90,30 @@ def modulated(O, rng, sf, S, F, amp=1.0, noise=0.0):
     return out
 
 
-@pytest.mark.parametrize("hw", [True, False])
 @pytest.mark.parametrize("sf", [6, 7, 8, 9, 10, 11, 12])
-def test_unscaled_frames(O, amd, sf, hw):
-    """max(|I|,|Q|) <= 1: the scale is 1 and the pre-pass estimate IS the exact one.  With
-    glibc sincosf in the demod (hw=False) every symbol is then exact as computed (nothing
-    to certify, nothing recomputed); with the hardware rotation (default) the symbols are
-    certified, and a frame whose estimated CFO sits near half a bin (two bins of almost
-    equal power in every data symbol, e.g. frame 5 at SF7 here) has a few recomputed."""
+def test_unscaled_frames(O, amd, sf):
+    """max(|I|,|Q|) <= 1: the scale is 1 and the pre-pass estimate IS the exact one; the
+    symbols (hardware rotation) are certified, and a frame whose estimated CFO sits near
+    half a bin (two bins of almost equal power in every data symbol, e.g. frame 5 at SF7
+    here) has a few recomputed."""
     rng = np.random.default_rng(100 + sf)
     iq = modulated(O, rng, sf, 8 if sf < 11 else 5, 6, amp=0.5, noise=0.05)
     assert np.abs(iq.view(np.float32)).max() <= 1.0
-    plan, fixed = check(O, amd, iq, sf, hw=hw)
+    plan, fixed = check(O, amd, iq, sf)
     assert plan.last_kernels() == SPEC
-    if hw:
-        assert fixed <= iq.shape[0] * (iq.shape[1] // (1 << sf) - 2) // 4
-    else:
-        assert fixed == 0
+    assert fixed <= iq.shape[0] * (iq.shape[1] // (1 << sf) - 2) // 4
 
 
-@pytest.mark.parametrize("hw", [True, False])
 @pytest.mark.parametrize("sf", [6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("snr_db", [20, 0, -10, -15])
-def test_rescaled_frames_match_oracle(O, amd, sf, snr_db, hw):
+def test_rescaled_frames_match_oracle(O, amd, sf, snr_db):
     """max > 1 (rescaled) at high and low SNR: certified or recomputed, always exact."""
     rng = np.random.default_rng(1000 * sf + snr_db + 50)
     amp = 2.5
     noise = amp * 10 ** (-snr_db / 20) / np.sqrt(2)
     iq = modulated(O, rng, sf, 10 if sf < 11 else 5, 8 if sf < 10 else 3, amp=amp, noise=noise)
     assert np.abs(iq.view(np.float32)).max() > 1.0
-    plan, fixed = check(O, amd, iq, sf, hw=hw)
+    plan, fixed = check(O, amd, iq, sf)
     assert plan.last_kernels() == SPEC
     assert fixed >= 0
 
@@ -262,7 +251,7 @@ def test_fast_precision_rescaled_frames_are_exact(O, amd, sf, snr_db):
         assert bits(res.time_offset[f].item()) == bits(otoff)
 
 
-@pytest.mark.parametrize("path", ["hw", "glibc", "split"])
+@pytest.mark.parametrize("path", ["spec", "split"])
 @pytest.mark.parametrize("sf,dechirp", [(7, True), (7, False), (9, True), (12, True)])
 def test_max_amp_is_the_reference_frame_maximum(O, amd, sf, dechirp, path):
     """max_amp (LoRaDemod.cpp:59-67: max of |I|, |Q| over the whole frame as handed to
@@ -289,13 +278,10 @@ def test_max_amp_is_the_reference_frame_maximum(O, amd, sf, dechirp, path):
         iq[f, S * N:] = (0.3 * rng.standard_normal(L - S * N)).astype(np.complex64)
     if path == "split":
         os.environ["LORA_MI355X_SPEC"] = "0"
-    if path == "glibc":
-        os.environ["LORA_MI355X_SPEC_HW"] = "0"
     try:
         plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=dechirp)
     finally:
         os.environ.pop("LORA_MI355X_SPEC", None)
-        os.environ.pop("LORA_MI355X_SPEC_HW", None)
     res = plan.run(torch.from_numpy(iq).cuda())
     torch.cuda.synchronize()
     assert ("spec" in plan.last_kernels()) == (path != "split")
