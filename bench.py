@@ -59,7 +59,9 @@ def _free_port() -> int:
 def spawn_ranks(argv, n):
     """Start `n` copies of this script as ranks 0..n-1 (children, not exec: this parent
     has not initialised the GPU and never does).  Rank 0's stdout is ours; the others'
-    stdout goes to stderr.  Returns the worst exit code."""
+    stdout goes to stderr.  Any rank that fails - a non-zero exit or a signal (negative
+    return code, e.g. SIGSEGV after a GPU fault) - fails the job, and the surviving ranks
+    are terminated instead of waiting in the gloo rendezvous.  Returns the exit code."""
     port = _free_port()
     procs = []
     for r in range(n):
@@ -71,8 +73,18 @@ def spawn_ranks(argv, n):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=None if r == 0 else sys.stderr.fileno()))
     rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
     return rc
 
 
@@ -100,7 +112,9 @@ def dist_setup(n_gpus, plumbing=False):
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")
+        import datetime
+
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
         return dist, dist.get_rank(), world, local
     return None, 0, 1, local
 
@@ -410,11 +424,15 @@ def fast_summary(r):
 
 
 def variant_summary(r, base, note):
-    return {"note": note, "ms_per_step": r["ms_per_step"], "stage_ms": r["stage_ms"],
+    """A data-dependent variant of a workload: `ratio_to_headline` is its time per data
+    symbol over the headline's (> 1 = slower)."""
+    return {"note": note, "frames": r["frames"], "data_symbols_per_frame": r["data_symbols"] // r["frames"],
+            "ms_per_step": r["ms_per_step"], "stage_ms": r["stage_ms"],
             "value_all_ranks_msym_s": r["msym_s_all_ranks"], "ser_vs_tx": r["ser_vs_tx"],
             "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS, "kernels": r["kernels"],
             "spec_recomputed_per_step": r["spec_recomputed_per_step"],
-            "ratio_to_headline": r["ms_per_step"] / base["ms_per_step"]}
+            "spec_recomputed_frac": r["spec_recomputed_per_step"] / r["data_symbols"],
+            "ratio_to_headline": base["msym_s_data"] / r["msym_s_data"]}
 
 
 def hbm_probe(device, nbytes=2 << 30, reps=5):
@@ -546,6 +564,18 @@ def main():
         extra["awgn_0db_sf7"] = variant_summary(rn, r7, "AWGN 0 dB (sigma/sqrt2 per component, "
                                                        "awgn_sweep_gtest.cpp:76-80); t_off != 0 frames")
         del rn
+        # the certified pipeline's worst case: near-ties at low SNR are recomputed exactly
+        rn = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, snr_db=-10.0,
+                        rank=rank)
+        extra["awgn_m10db_sf7"] = variant_summary(rn, r7, "AWGN -10 dB: symbol errors and near-ties; symbols "
+                                                         "failing certification are recomputed exactly")
+        del rn
+        # a 255-byte payload: 510 data symbols per frame (lora_encode: 2 symbols per byte)
+        long_frames = max(1, args.frames * args.data_symbols // 510)
+        rl = run_config(7, long_frames, 510, args.steps, args.warmup, dist, device, rank=rank)
+        extra["long_frames_sf7"] = variant_summary(rl, r7, "255-byte payload: 2 + 510 symbols per frame, "
+                                                          "noiseless, same data symbols per step")
+        del rl
         torch.cuda.empty_cache()
         extra["mod_sf7"] = run_modulator(7, args.frames, args.data_symbols, device)
     r12 = None
@@ -565,6 +595,19 @@ def main():
                 extra["sf12"]["cpu_baseline"] = cpu_baseline(12, r12["iq"], args.data_symbols, 64)
             except Exception as e:  # the CPU leg must not kill the GPU measurement
                 log("sf12 cpu baseline failed:", e)
+        if not args.no_variants:
+            # noisy copy of the same batch, generated in place (no second 33.8 GB buffer)
+            sigma = 10.0 ** (10.0 / 20.0) / math.sqrt(2.0)
+            gn = torch.Generator(device=device).manual_seed(77)
+            iqn = r12["iq"]
+            for r0 in range(0, iqn.shape[0], 512):
+                blk = iqn[r0:r0 + 512]
+                blk += torch.view_as_complex(torch.randn(blk.shape + (2,), generator=gn, device=device)) * sigma
+            r12n = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 4, 2), args.warmup,
+                              dist, device, inputs=(r12["syms"], iqn), rank=rank)
+            extra["awgn_m10db_sf12"] = variant_summary(r12n, r12, "AWGN -10 dB on the SF12 batch: symbol errors "
+                                                                  "and near-ties, recomputed exactly")
+            del r12n
         del r12
         torch.cuda.empty_cache()
         if not args.no_variants:

@@ -115,12 +115,15 @@ int lora_demod_plan_destroy(lora_demod_plan* plan);
  * (LORA_MODE_API: frame_len must be a multiple of N*osr with >= 2 symbols). */
 int64_t lora_demod_symbols_per_frame(const lora_demod_plan* plan, int64_t frame_len);
 
-/* Device workspace bytes lora_demod_batch needs for `frames` frames (0 allowed). */
-size_t lora_demod_workspace_bytes(const lora_demod_plan* plan, int64_t frames);
+/* Device workspace bytes lora_demod_batch needs for `frames` frames of `frame_len`
+ * samples (0 when frames is 0).  The reference's workspace is caller-owned too
+ * (lora_demod_workspace, phy.hpp:170-185, plus its scratch buffer sized to the frame). */
+size_t lora_demod_workspace_bytes(const lora_demod_plan* plan, int64_t frames, int64_t frame_len);
 
 /* Demodulate `frames` frames of `frame_len` complex samples each, frame f starting
  * at iq + 2*f*frame_stride floats.  `workspace` must hold
- * lora_demod_workspace_bytes(plan, frames) bytes of device memory (may be NULL if 0).
+ * lora_demod_workspace_bytes(plan, frames, frame_len) bytes of device memory (may be NULL
+ * if 0).
  * Returns symbols per frame (>= 0) or a negative error. */
 int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
                          int64_t frame_len, int64_t frame_stride, const lora_demod_outputs* out,
@@ -177,8 +180,8 @@ int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls);
 #define LORA_KERNEL_SPEC 64 /* the speculative single-read pipeline (with ESTIMATE + DEMOD) */
 int lora_demod_last_kernels(const lora_demod_plan* plan);
 
-/* LEGACY frames at osr 1 without a window, SF 6-12, 3..80 symbols, run as a speculative
- * single-read pipeline (LORA_KERNEL_SPEC): the offset estimate on unscaled samples, every
+/* LEGACY frames at osr 1 without a window, SF 6-12, of 3 .. 2 + 4 * 2^SF symbols (SF7: 514),
+ * run as a speculative single-read pipeline (LORA_KERNEL_SPEC): the offset estimate on unscaled samples, every
  * data symbol demodulated once while the frame maximum is reduced from the same read, then
  * the exact estimate, with each data symbol either certified by a rounding bound on its
  * argmax margin or recomputed exactly - the outputs equal the reference's (LoRaDemod.cpp:

@@ -1,32 +1,44 @@
 /*
- * lora_mi355x_phy.hpp — C++ drop-in for the reference's legacy demodulator API, over the
+ * lora_mi355x_phy.hpp — C++ drop-in for the reference's <lora_phy/phy.hpp> API, over the
  * C-ABI of lora_mi355x.h (the same liblora_mi355x.so exports both).
  *
- * A caller written against the reference's <lora_phy/phy.hpp> legacy helpers and
- * <lora_phy/ChirpGenerator.hpp> genChirp (e.g. tests/e2e_chain_test.cpp:54-117) compiles
+ * A caller written against the reference's phy.hpp and <lora_phy/ChirpGenerator.hpp>
+ * (e.g. tests/e2e_chain_test.cpp:54-117, runners/rx_runner.cpp:102-122) compiles
  * unchanged with -I<repo>/include/compat (whose lora_phy/phy.hpp and
  * lora_phy/ChirpGenerator.hpp only include this header) and links with -llora_mi355x.
  * The functions keep the reference's names, argument meaning and return values; the
  * demodulation runs on the GPU:
  *
+ *   workspace API (phy.hpp:96-156, src/phy/phy.cpp:26-261)
+ *   init / reset                          phy.hpp:102-106, phy.cpp:26-53
+ *   encode / decode                       phy.hpp:111-121, phy.cpp:55-63, 241-256
+ *   modulate                              phy.hpp:126-128, phy.cpp:65-76
+ *   demodulate                            phy.hpp:134-136, phy.cpp:178-239
+ *   estimate_offsets / compensate_offsets phy.hpp:142-152, phy.cpp:78-176
+ *   get_last_metrics                      phy.hpp:156, phy.cpp:258-261
+ *   legacy helpers (phy.hpp:158-215)
  *   lora_demod_init / lora_demod_free     phy.hpp:190-194, LoRaDemod.cpp:10-47
  *   lora_demodulate                       phy.hpp:204-207, LoRaDemod.cpp:49-195
  *   lora_modulate                         phy.hpp:198-201, LoRaMod.cpp:8-41
  *   lora_encode / lora_decode             phy.hpp:210-215, LoRaEncoder.cpp / LoRaDecoder.cpp
  *   genChirp (float)                      ChirpGenerator.hpp:24-50
  *
- * Source-compatible, not binary-compatible: lora_demod_workspace has the reference's
- * name and the fields callers touch (N, window_kind, metrics, scratch, scratch_len), but
- * holds a device plan and device buffers instead of kissfft state.  Ownership follows
- * the reference: the caller owns the workspace object and the scratch buffer; the
- * device resources the workspace holds are created by lora_demod_init (sized by its
- * max_samples) and released by lora_demod_free.  lora_demodulate allocates only when a
- * call exceeds the max_samples given to init (or init was given none).  Host pointers in,
- * host pointers out; each call is synchronous like the reference's.  For batches of
- * frames already in device memory use lora_demod_batch (lora_mi355x.h) directly.
+ * Source-compatible, not binary-compatible: lora_workspace and lora_demod_workspace have
+ * the reference's names and every field callers touch, but hold a device plan, device
+ * buffers and pinned host staging instead of kissfft state.  Ownership follows the
+ * reference: the caller owns the workspace object and its buffers (symbol_buf, fft_in,
+ * fft_out, window, scratch); the device resources are created by init / lora_demod_init
+ * and released by lora_demod_free or, for lora_workspace (whose reference API has no free
+ * call), by its destructor.  Neither workspace may be copied.  Each call is synchronous,
+ * host pointers in and out, like the reference's; lora_demodulate performs no host
+ * allocation when the frame fits the max_samples given to lora_demod_init (the
+ * reference's no_alloc_test.cpp:90-99 guard).  For batches of frames already in device
+ * memory use lora_demod_batch (lora_mi355x.h) directly.
  */
 #ifndef LORA_MI355X_PHY_HPP
 #define LORA_MI355X_PHY_HPP
+
+#include <sys/types.h>
 
 #include <cmath>
 #include <complex>
@@ -53,12 +65,77 @@ enum class bandwidth : unsigned {
 constexpr float bw_to_hz(bandwidth bw) { return static_cast<float>(static_cast<unsigned>(bw)); }
 constexpr float bw_scale(bandwidth bw) { return bw_to_hz(bw) / 125000.0f; }
 
+/* phy.hpp:51-58 */
+struct lora_params {
+  unsigned sf{};
+  bandwidth bw{bandwidth::bw_125};
+  unsigned cr{};
+  unsigned osr{1};
+  window_type window{window_type::window_none};
+  uint8_t sync_word{0x12};
+};
+
 /* phy.hpp:65-69 */
 struct lora_metrics {
   bool crc_ok{};
   float cfo{};
   float time_offset{};
 };
+
+namespace detail {
+/* Device side of a workspace: an API- or LEGACY-mode plan, one device allocation (IQ |
+ * symbols | per-frame outputs | batch workspace), pinned host staging for the same
+ * layout, and a stream. */
+struct device_state {
+  unsigned sf{};
+  unsigned plan_osr{};
+  int plan_window{-1};
+  unsigned plan_bw{};
+  int device{};
+  ::lora_demod_plan* plan{};
+  void* dev{};
+  void* host{};
+  size_t bytes{};    // capacity of dev and host
+  size_t samples{};  // IQ capacity in complex samples
+  void* stream{};    // hipStream_t
+};
+void release(device_state& d);
+}  // namespace detail
+
+/* phy.hpp:77-92 (same name and caller-visible fields; device state instead of kissfft
+ * plans).  Released by its destructor: the reference's workspace API has no free call. */
+struct lora_workspace {
+  uint16_t* symbol_buf{};
+  std::complex<float>* fft_in{};
+  std::complex<float>* fft_out{};
+  float* window{};
+  window_type window_kind{window_type::window_none};
+  lora_metrics metrics{};
+  unsigned osr{1};
+  bandwidth bw{bandwidth::bw_125};
+  uint8_t sync_word{0x12};
+  // device side, owned between init and destruction
+  detail::device_state gpu{};
+
+  lora_workspace() = default;
+  lora_workspace(const lora_workspace&) = delete;
+  lora_workspace& operator=(const lora_workspace&) = delete;
+  ~lora_workspace() { detail::release(gpu); }
+};
+
+int init(lora_workspace* ws, const lora_params* cfg);
+void reset(lora_workspace* ws);
+ssize_t encode(lora_workspace* ws, const uint8_t* payload, size_t payload_len, uint16_t* symbols,
+               size_t symbol_cap);
+ssize_t decode(lora_workspace* ws, const uint16_t* symbols, size_t symbol_count, uint8_t* payload,
+               size_t payload_cap);
+ssize_t modulate(lora_workspace* ws, const uint16_t* symbols, size_t symbol_count, std::complex<float>* iq,
+                 size_t iq_cap);
+ssize_t demodulate(lora_workspace* ws, const std::complex<float>* iq, size_t sample_count, uint16_t* symbols,
+                   size_t symbol_cap);
+void estimate_offsets(lora_workspace* ws, const std::complex<float>* samples, size_t sample_count);
+void compensate_offsets(const lora_workspace* ws, std::complex<float>* samples, size_t sample_count);
+const lora_metrics* get_last_metrics(const lora_workspace* ws);
 
 /* phy.hpp:170-185 (same name and caller-visible fields; device state instead of kissfft) */
 struct lora_demod_workspace {
@@ -68,13 +145,7 @@ struct lora_demod_workspace {
   std::complex<float>* scratch{};
   size_t scratch_len{};
   // device side, owned between lora_demod_init and lora_demod_free
-  unsigned sf{};
-  unsigned plan_osr{};
-  int device{};
-  ::lora_demod_plan* plan{};
-  void* dev{};          // one device allocation: IQ | symbols | per-frame outputs | workspace
-  size_t dev_samples{};  // IQ capacity of `dev` in complex samples
-  void* stream{};        // hipStream_t
+  detail::device_state gpu{};
 };
 
 void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win = window_type::window_none,

@@ -122,18 +122,31 @@ float bw_scale_of(unsigned bw_hz) { return static_cast<float>(bw_hz) / 125000.0f
 
 bool bw_ok(unsigned bw) { return bw == 125000 || bw == 250000 || bw == 500000; }
 
-// Workspace: per-frame partial maxima (written by k_frame_max, no zeroing pass), then
-// per-frame FrameParams.
-size_t ws_counter_bytes(int64_t frames) {  // partial maxima, kMaxBpf per frame
-  return ((size_t)frames * lora::kMaxBpf * sizeof(uint32_t) + 255) & ~size_t(255);
+// k_frame_max blocks per frame: rounded DOWN, so each block streams at least one full
+// batch of 4096 samples (256 threads x 8 pairs): SF7 frames of 8448 samples as 2 x 4224
+// rather than 3 x 2816 (partly idle batches); SF12 66 x 4096; at most kMaxBpf (longer
+// frames use longer blocks).
+constexpr int kMaxChunk = 4096;
+int frame_max_blocks(int64_t frame_len) {
+  return frame_len > 0 ? (int)std::min<int64_t>(lora::kMaxBpf, std::max<int64_t>(1, frame_len / kMaxChunk)) : 1;
 }
-size_t ws_params_bytes(int64_t frames) {  // FrameParams per frame
-  return ((size_t)frames * sizeof(lora::FrameParams) + 255) & ~size_t(255);
-}
-// speculative pipeline: pre-pass FrameParams + (margin, window max) per data symbol
-// (<= kMaxBpf - 1 of them)
-size_t ws_spec_bytes(int64_t frames) {
-  return ws_params_bytes(frames) + (((size_t)frames * (lora::kMaxBpf - 1) * 2 * sizeof(float) + 255) & ~size_t(255));
+
+// Workspace of one lora_demod_batch call, sized from the frames (no zeroing pass, no
+// atomics on it): per-frame partial maxima (k_frame_max blocks; the speculative pipeline
+// uses the first slot), the exact FrameParams, the pre-pass FrameParams and one
+// (margin, window max) pair per data symbol.
+struct WsLayout {
+  size_t fp, fp_spec, marg, total;
+};
+WsLayout ws_layout(int64_t frames, int64_t frame_len, int step) {
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const int64_t per = std::max<int64_t>(0, frame_len / step - 2);
+  WsLayout w;
+  w.fp = al((size_t)frames * frame_max_blocks(frame_len) * sizeof(uint32_t));
+  w.fp_spec = w.fp + al((size_t)frames * sizeof(lora::FrameParams));
+  w.marg = w.fp_spec + al((size_t)frames * sizeof(lora::FrameParams));
+  w.total = w.marg + al((size_t)frames * per * 2 * sizeof(float));
+  return w;
 }
 
 // ---------------------------------------------------------------------------------
@@ -884,10 +897,9 @@ int64_t lora_demod_symbols_per_frame(const lora_demod_plan* plan, int64_t frame_
   return total >= 2 ? total - 2 : total;  // LoRaDemod.cpp:194
 }
 
-size_t lora_demod_workspace_bytes(const lora_demod_plan* plan, int64_t frames) {
-  (void)plan;
-  if (frames <= 0) return 0;
-  return ws_counter_bytes(frames) + ws_params_bytes(frames) + ws_spec_bytes(frames);
+size_t lora_demod_workspace_bytes(const lora_demod_plan* plan, int64_t frames, int64_t frame_len) {
+  if (!plan || frames <= 0 || frame_len < 0) return 0;
+  return ws_layout(frames, frame_len, plan->step).total;
 }
 
 int64_t lora_demod_spec_recomputed(lora_demod_plan* plan) {
@@ -910,7 +922,8 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   if (!iq) return set_error(LORA_EINVAL, "null iq");
   if (out->symbols && out->sym_stride < nsym)
     return set_error(LORA_ERANGE, "sym_stride smaller than symbols per frame");  // phy.cpp:190
-  const size_t need = lora_demod_workspace_bytes(plan, frames);
+  const WsLayout wl = ws_layout(frames, frame_len, plan->step);
+  const size_t need = wl.total;
   if (!workspace || workspace_bytes < need)
     return set_error(LORA_ERANGE, "workspace too small");
 
@@ -947,9 +960,9 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   unsigned char* wsb = static_cast<unsigned char*>(workspace);
   uint32_t* maxbits = reinterpret_cast<uint32_t*>(wsb);
   a.maxbits = maxbits;
-  a.fp = reinterpret_cast<lora::FrameParams*>(wsb + ws_counter_bytes(frames));
-  a.fp_spec = reinterpret_cast<lora::FrameParams*>(wsb + ws_counter_bytes(frames) + ws_params_bytes(frames));
-  a.spec_marg = reinterpret_cast<float*>(wsb + ws_counter_bytes(frames) + 2 * ws_params_bytes(frames));
+  a.fp = reinterpret_cast<lora::FrameParams*>(wsb + wl.fp);
+  a.fp_spec = reinterpret_cast<lora::FrameParams*>(wsb + wl.fp_spec);
+  a.spec_marg = reinterpret_cast<float*>(wsb + wl.marg);
   a.spec_max = maxbits;
   a.spec_fix = plan->spec_fix;
   a.syms = out->symbols;
@@ -963,13 +976,8 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
 
   const int s0 = a.have_sync ? 2 : 0;
   const int64_t per = total - s0;
-  // k_frame_max: blocks per frame rounded DOWN, so each block streams at least one full
-  // batch of 4096 samples (256 threads x 8 pairs): SF7 frames of 8448 samples as 2 x 4224
-  // rather than 3 x 2816 (partly idle batches); SF12 66 x 4096.  Frames shorter than two
-  // batches take one wave each (k_frame_max_wave).
-  constexpr int kMaxChunk = 4096;
-  const int bpf = frame_len > 0 ? (int)std::min<int64_t>(lora::kMaxBpf, std::max<int64_t>(1, frame_len / kMaxChunk))
-                                : 1;
+  // k_frame_max: frames shorter than two batches take one wave each (k_frame_max_wave)
+  const int bpf = frame_max_blocks(frame_len);
   const bool max_wave = bpf == 1;
   a.mx_bpf = (p.mode == LORA_MODE_LEGACY && frame_len > 0) ? bpf : 0;
   // split evenly over the frame's blocks
@@ -1002,7 +1010,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   // recomputations.  The symbol demod rotates with the hardware sine/cosine under either
   // precision; the certification holds it to the EXACT reference.
   const bool spec_ok = plan->spec && p.mode == LORA_MODE_LEGACY && p.osr == 1 && !a.hann && p.sf >= 6 &&
-                       total >= 3 && total - 2 + 1 <= lora::kMaxBpf;
+                       total >= 3 && total - 2 <= lora::kSpecChunks * (plan->N / 16);
   if (rc == LORA_OK && spec_ok) {
     KArgs as = a;
     as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows

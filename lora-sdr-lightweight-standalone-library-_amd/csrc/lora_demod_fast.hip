@@ -790,7 +790,9 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint64_t red[4];
   __shared__ FrameParams sp[SPB];
-  __shared__ unsigned long long fmask[SPEC == 2 ? SPB : 1][2];
+  // SPEC == 2: per frame group, one bit per data symbol that failed certification
+  // (frames of up to kSpecChunks * T data symbols)
+  __shared__ unsigned long long fmask[SPEC == 2 ? SPB : 1][SPEC == 2 ? T : 1];
   const int tid = threadIdx.x;
   const int step = DYN ? a.step : N;
   const int osr = DYN ? a.osr : 1;
@@ -805,20 +807,17 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   const cf* __restrict__ x = a.iq + f * a.frame_stride;
   cf* row = reinterpret_cast<cf*>(smem) + (size_t)g * rowc;
   // LoRaDemod.cpp:59-67 max_amp from the frame's partials: the group's lanes load them
-  // in parallel (up to kMaxBpf, one dependent load chain per lane is latency-bound)
+  // in parallel (one dependent load chain per lane is latency-bound)
   float maxv = 0.0f;
-  constexpr int NPL = (kMaxBpf + T - 1) / T;  // SPEC == 2: data symbols per lane, at most
   if (legacy && SPEC != 1) {
     if constexpr (SPEC == 2) {
       // the pre-pass's slot (samples outside the data windows) and every data window's
-      // maximum from the demod's (margin, max) pairs; all loads issued together
+      // maximum from the demod's (margin, max) pairs, eight loads in flight per lane
       maxv = __uint_as_float(a.maxbits[f]);
       const int per = a.total - 2;
-#pragma unroll
-      for (int i = 0; i < NPL; ++i) {
-        const int j = l + i * T;
-        if (j < per) maxv = fmaxf(maxv, a.spec_marg[2 * (f * per + j) + 1]);
-      }
+      const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
+#pragma unroll 8
+      for (int j = l; j < per; j += T) maxv = fmaxf(maxv, mg[j].y);
     } else {
       for (int c = l; c < a.mx_bpf; c += T) maxv = fmaxf(maxv, __uint_as_float(a.maxbits[f * a.mx_bpf + c]));
     }
@@ -1081,70 +1080,65 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   }  // exact estimate
   if constexpr (SPEC == 2) {
     // ---- certification of the data symbols the demod computed speculatively ----
-    // The demod used the pre-pass offsets qs on unscaled samples y; the reference uses q
-    // on y * scale.  In exact arithmetic the two spectra differ by the factor `scale` and
-    // the rotation difference; every fp32 rounding of the chain (the product y * scale,
-    // the phase start + rate * i, sincosf, the rotation product, kissfft's butterflies,
-    // |X|^2) perturbs a bin by at most E * sum_i |y_i| with E = (8 log2 N + 32) * 2^-24
-    // (the FFT's per-stage error is bounded by its partial sums <= sum_i |y_i|), and a
-    // phase difference d(phi) by at most d(phi) * sum_i |y_i|.  So if the speculative
-    // top bin exceeds the runner-up by more than twice the bound (times 2 for safety),
-    // the reference's argmax is the same bin, strictly (no tie).  Otherwise - or when the
-    // two estimates disagree on t_off - the symbol is recomputed exactly below.
+    // The demod used the pre-pass offsets qs (rate r', t_off) on the unscaled samples y;
+    // the reference uses q (rate r, the same t_off, else the symbol is recomputed) on
+    // fl(y * scale).  Argmax ignores the positive factor `scale`, so compare the
+    // reference's spectrum with scale x the demod's, bin by bin, for data symbol s = 2 + j
+    // (window of N points i, phase argument A + i with A = s N + t_off):
+    //  * the reference's phase fl(fl(r fl(A)) + fl(r i)) is within u (rmax L) of
+    //    r (A + i) for each of its three roundings (A, the product, the sum; L = (s + 1) N
+    //    + |t_off| >= |A + i|) plus u rmax N for fl(r i): e_ref = 3 u rmax L + u rmax N;
+    //  * the demod's factor of point i = l + T q is the hardware sin/cos of
+    //    fract(fl(ph0 fl(1/2pi))) for the lane's first point (ph0 rounded like the
+    //    reference's phase: 3 u rmax L + u rmax N; the product by fl(1/2pi): 2 u rmax L;
+    //    v_sin/v_cos_f32 within 1.26e-7 of sin/cos(2 pi x) for every fp32 x in [0, 1),
+    //    measured exhaustively by tools/micro/hw_sincos_err.hip), then 15 steps of a fused
+    //    complex product by the step factor w = e^{i r' T} (hardware sin/cos of
+    //    fract(fl(fl(r' T) fl(1/2pi))), T a power of two: within 2 u rmax T + 1.8e-7 of
+    //    e^{i r' T}, and each product rounds by <= 2 sqrt2 u): e_spec = 5 u rmax L +
+    //    u rmax N + 2 sqrt2 1.26e-7 + 15 (2 u rmax T + 1.8e-7 + 2 sqrt2 u) < 5 u rmax L +
+    //    u rmax N + 6e-6;
+    //  * the two exact phases differ by |r - r'| L;
+    //  * every other rounding (the product y * scale, the rotation product, log2 N
+    //    butterfly stages with table twiddles, |X|^2 and its square root) moves a bin by
+    //    at most E sum_i |y_i| per path, E = (8 log2 N + 32) u (a stage's rounding is
+    //    bounded by its partial sums <= sum_i |y_i|).
+    // With n1 = 2 N max(|re|, |im|) over the window >= sum_i |y_i|, each bin moves by less
+    // than B = n1 (|r - r'| L + e_ref + e_spec + 2 E) between the paths, so a speculative
+    // top bin ahead of the runner-up by d > 2 B is the reference's argmax, strictly (no
+    // tie to break).  The kernel requires d > 4 B; a symbol that fails is recomputed
+    // exactly below with the reference's arithmetic (lora_demod_spec_recomputed() counts
+    // them).
     const FrameParams qs = a.fp_spec[f];
     const int per = a.total - 2;
     const bool same_t = qs.t_off == q.t_off;
-    if (l < 2) fmask[g][l] = 0;
+    for (int w = l; w < T; w += T) fmask[g][w] = 0;
     block_sync<G::WAVE_LOCAL>();
-    {  // rescaled frames only (the others left above)
-      const double eps = 1.0 / 16777216.0;
-      const double E = (8.0 * SF + 32.0) * eps;
+    {
+      const double u = 1.0 / 16777216.0;
+      const double E = (8.0 * SF + 32.0) * u;
       const double drate = fabs((double)q.rate - (double)qs.rate);
       const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
       const double tabs = (double)abs(q.t_off);
-      uint32_t bad = 0;  // bit i: symbol l + i*T failed (all loads issued before any test)
-#pragma unroll
-      for (int i = 0; i < NPL; ++i) {
-        const int j = l + i * T;
-        if (j < per) {
-          const float2 v = reinterpret_cast<const float2*>(a.spec_marg)[f * per + j];
-          const float d = v.x;
-          // sum_i |y_i| <= sum_i (|re_i| + |im_i|) <= 2 N max(|re|, |im|) over the window
-          const double n1 = 2.0 * N * (double)v.y;
-          const double L = (double)(2 + j) * N + tabs + N;  // |phase argument| scale of symbol 2+j
-          // Hardware rotation: the demod rotated by
-          // v_sin/v_cos_f32 of fract(fl(ph * fl(1/2pi))) instead of glibc sincosf(ph): the
-          // argument's two roundings move the angle by <= 2 eps |ph| rad, and the unit itself
-          // is within 1.26e-7 of sin/cos(2 pi r) for every fp32 r in [0, 1) (measured
-          // exhaustively, tools/micro/hw_sincos_err.hip), so each rotation factor is off by
-          // < 2 eps |ph| + sqrt(2) * 1.26e-7; doubled here.  That demod also computes its
-          // complex products with fused multiply-adds: one rounding where the reference has
-          // two, so E bounds its FFT and products as well.  Certified against the exact
-          // reference like every other symbol.
-          // The demod takes one such factor r0 per lane (its first point)
-          // and one w for the step rate*T, then r_{q+1} = fma-product(r_q, w) for the lane's
-          // P = 16 points: |r_q - e^{i phi_q}| <= E_0 + q (e_w + 2 sqrt2 eps), with
-          // E_0 <= 2 eps |ph_0| + sqrt2 * 1.26e-7 and e_w <= 2 eps |rate T| + sqrt2 * 1.26e-7
-          // (|r|, |w| within 3e-6 of 1), so every factor is off by < 2 eps rmax L + 5.4e-6
-          // (|ph_0| + 15 |rate| T <= rmax L); doubled here.
-          const double hwd = 1.1e-5;
-          const double fastd = 4.0 * eps * rmax * L + hwd;
-          const double B = n1 * (drate * L + 6.0 * eps * rmax * L + 2.0 * E + fastd);
-          if (!(same_t && (double)d > 4.0 * B)) bad |= 1u << i;
-        }
+      const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
+#pragma unroll 8
+      for (int j = l; j < per; j += T) {
+        const float2 v = mg[j];
+        const double n1 = 2.0 * N * (double)v.y;
+        const double L = (double)(3 + j) * N + tabs;
+        const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
+        const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 6e-6;
+        const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
+        if (!(same_t && (double)v.x > 4.0 * B)) atomicOr(&fmask[g][j >> 6], 1ull << (j & 63));
       }
-      for (int i = 0; i < NPL; ++i)
-        if (bad >> i & 1) {
-          const int j = l + i * T;
-          atomicOr(&fmask[g][j >> 6], 1ull << (j & 63));
-        }
     }
     block_sync<G::WAVE_LOCAL>();
-    const unsigned long long fm0 = fmask[g][0], fm1 = fmask[g][1];
-    if (fm0 | fm1) {
-      cf in[P], z[P];
-      for (int j = 0; j < per; ++j) {
-        if (!(((j < 64) ? fm0 >> j : fm1 >> (j - 64)) & 1)) continue;  // group-uniform
+    cf in[P], z[P];
+    for (int w = 0; w < (per + 63) >> 6; ++w) {  // group-uniform: every lane reads the same words
+      unsigned long long m = fmask[g][w];
+      while (m) {
+        const int j = w * 64 + __builtin_ctzll(m);
+        m &= m - 1;
         const int s = 2 + j;
         int64_t base;
         int cg;

@@ -6,9 +6,13 @@
 
 namespace lora {
 
-// Partial maxima per frame kept in the workspace (no zeroing pass, no atomics); frames
-// longer than kMaxBpf * 4096 samples use proportionally longer blocks.
+// Partial maxima per frame kept in the workspace by k_frame_max (no zeroing pass, no
+// atomics); frames longer than kMaxBpf * 4096 samples use proportionally longer blocks.
 constexpr int kMaxBpf = 80;  // SF12 frames of 66 symbols: 66 blocks of 4096 samples
+// Speculative pipeline: a frame of up to kSpecChunks * T data symbols (T = N/16 lanes per
+// symbol; SF6 256, SF7 512, ..., SF12 16384), one certification bit per data symbol in the
+// certify kernel's LDS.
+constexpr int kSpecChunks = 64;
 
 struct KArgs {
   const cf* iq;

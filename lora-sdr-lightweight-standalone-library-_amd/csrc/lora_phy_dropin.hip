@@ -1,6 +1,6 @@
-// lora_phy_dropin.hip — the reference's legacy C++ API (include/lora_mi355x_phy.hpp)
-// implemented on the C-ABI: one frame per call, host buffers in and out, the demodulation
-// on the plan's device.  Reference semantics kept per function (file:line in the header).
+// lora_phy_dropin.hip — the reference's C++ API (include/lora_mi355x_phy.hpp) implemented
+// on the C-ABI: one frame per call, host buffers in and out, the demodulation on the
+// plan's device.  Reference semantics kept per function (file:line in the header).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,13 +35,40 @@ uint8_t dec_h84_nibble(uint8_t b) {
   }
 }
 
-// Per-frame outputs and the batch workspace behind the IQ in the workspace's single
-// device allocation.
+// SX1272 payload CRC of LoRaCodes.hpp:69-105: a CCITT shift register (polynomial 0x1021)
+// over the bytes, its output masked with an 8-bit LFSR (taps 0xB8) stepped once per byte
+// and once more for the high byte.
+uint16_t sx1272_data_checksum(const uint8_t* data, int length) {
+  auto parity = [](uint8_t t) {
+    t ^= t >> 4;
+    t ^= t >> 2;
+    t ^= t >> 1;
+    return (uint8_t)(t & 1);
+  };
+  auto shift8 = [](uint16_t c) {
+    for (int i = 0; i < 8; ++i) c = (c & 0x8000) ? (uint16_t)((c << 1) ^ 0x1021) : (uint16_t)(c << 1);
+    return c;
+  };
+  uint16_t res = 0;
+  uint8_t v = 0xff;
+  for (int i = 0; i < length; ++i) {
+    const uint16_t crc = shift8(res);
+    v = (uint8_t)(parity(v & 0xB8) | (v << 1));
+    res = (uint16_t)(crc ^ data[i]);
+  }
+  res ^= v;
+  v = (uint8_t)(parity(v & 0xB8) | (v << 1));
+  res ^= (uint16_t)(v << 8);
+  return res;
+}
+
+size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+// One frame's IQ, symbols and per-frame outputs, then the batch workspace: the same
+// layout in the device allocation and in the pinned host staging.
 struct DevLayout {
   size_t iq, syms, sync, cfo, toff, maxa, ws, total;
 };
-
-size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
 DevLayout layout(const lora_demod_plan* plan, size_t samples, size_t N) {
   DevLayout d;
@@ -59,82 +86,172 @@ DevLayout layout(const lora_demod_plan* plan, size_t samples, size_t N) {
   d.maxa = o;
   o += 256;
   d.ws = o;
-  o += align256(lora_demod_workspace_bytes(plan, 1));
+  o += align256(lora_demod_workspace_bytes(plan, 1, (int64_t)samples));
   d.total = o;
   return d;
 }
 
-// The plan for this call's oversampling (the reference passes osr per call): created on
-// first use, recreated when osr changes.
-bool ensure_plan(lora_phy::lora_demod_workspace* ws, unsigned osr) {
-  if (ws->plan && ws->plan_osr == osr) return true;
-  if (ws->plan) lora_demod_plan_destroy(ws->plan);
-  ws->plan = nullptr;
+// The plan for (sf, osr, window, bw, mode): kept while they match, recreated (the old one
+// destroyed) otherwise.  The reference passes osr per lora_demodulate call.
+bool ensure_plan(lora_phy::detail::device_state& g, unsigned sf, unsigned osr, int window, unsigned bw_hz,
+                 int mode) {
+  if (g.plan && g.sf == sf && g.plan_osr == osr && g.plan_window == window && g.plan_bw == bw_hz) return true;
+  if (g.plan) lora_demod_plan_destroy(g.plan);
+  g.plan = nullptr;
   lora_demod_params p{};
-  p.sf = ws->sf;
+  p.sf = sf;
   p.osr = osr;
-  p.bw_hz = 125000;  // no dechirp in the plan: the bandwidth only sets table phases it does not use
-  p.window = ws->window_kind == lora_phy::window_type::window_hann ? LORA_WINDOW_HANN : LORA_WINDOW_NONE;
-  p.dechirp = 0;     // lora_demodulate takes dechirped samples (its callers dechirp first)
-  p.mode = LORA_MODE_LEGACY;
-  p.device = ws->device;
+  p.bw_hz = bw_hz;
+  p.window = window;
+  p.dechirp = 0;  // lora_demodulate takes dechirped samples (its callers dechirp first)
+  p.mode = mode;
+  p.device = g.device;
   p.precision = LORA_PRECISION_EXACT;
-  if (lora_demod_plan_create(&p, &ws->plan) != LORA_OK) {
-    ws->plan = nullptr;
+  if (lora_demod_plan_create(&p, &g.plan) != LORA_OK) {
+    g.plan = nullptr;
     return false;
   }
-  ws->plan_osr = osr;
+  g.sf = sf;
+  g.plan_osr = osr;
+  g.plan_window = window;
+  g.plan_bw = bw_hz;
   return true;
 }
 
-bool ensure_dev(lora_phy::lora_demod_workspace* ws, size_t samples) {
-  if (ws->dev && ws->dev_samples >= samples) return true;
-  if (ws->dev) hipFree(ws->dev);
-  ws->dev = nullptr;
-  ws->dev_samples = 0;
-  const DevLayout d = layout(ws->plan, samples, ws->N);
-  if (hipMalloc(&ws->dev, d.total) != hipSuccess) {
-    ws->dev = nullptr;
+// Device buffer and pinned host staging for frames of up to `samples` samples with the
+// current plan (its osr sets the workspace size): grown, never shrunk.
+bool ensure_buffers(lora_phy::detail::device_state& g, size_t samples) {
+  const size_t want = std::max(samples, g.samples);
+  const DevLayout d = layout(g.plan, want, size_t(1) << g.sf);
+  if (g.dev && g.host && g.bytes >= d.total && g.samples >= samples) return true;
+  if (g.stream) hipStreamSynchronize(static_cast<hipStream_t>(g.stream));
+  if (g.dev) hipFree(g.dev);
+  if (g.host) hipHostFree(g.host);
+  g.dev = g.host = nullptr;
+  g.bytes = g.samples = 0;
+  if (hipMalloc(&g.dev, d.total) != hipSuccess) {
+    g.dev = nullptr;
     return false;
   }
-  ws->dev_samples = samples;
+  if (hipHostMalloc(&g.host, d.total, hipHostMallocDefault) != hipSuccess) {
+    hipFree(g.dev);
+    g.dev = g.host = nullptr;
+    return false;
+  }
+  g.bytes = d.total;
+  g.samples = want;
   return true;
+}
+
+bool ensure_stream(lora_phy::detail::device_state& g) {
+  if (g.stream) return true;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+  g.stream = st;
+  return true;
+}
+
+struct FrameOut {
+  int64_t nsym;
+  uint8_t sync;
+  float cfo, toff, max_amp;
+  const uint16_t* syms;  // in the pinned staging
+};
+
+// One frame through lora_demod_batch: host samples -> pinned staging -> device, the
+// kernels, outputs -> pinned staging, synchronise.  No host allocation.
+bool run_frame(lora_phy::detail::device_state& g, const std::complex<float>* samples, size_t count, FrameOut& out) {
+  hipStream_t st = static_cast<hipStream_t>(g.stream);
+  const DevLayout d = layout(g.plan, g.samples, size_t(1) << g.sf);
+  unsigned char* dev = static_cast<unsigned char*>(g.dev);
+  unsigned char* host = static_cast<unsigned char*>(g.host);
+  const int64_t nsym = lora_demod_symbols_per_frame(g.plan, (int64_t)count);
+  if (nsym < 0) return false;
+  if (count > 0) {
+    if (samples != reinterpret_cast<const std::complex<float>*>(host + d.iq))
+      std::memcpy(host + d.iq, samples, count * sizeof(std::complex<float>));
+    if (hipMemcpyAsync(dev + d.iq, host + d.iq, count * sizeof(std::complex<float>), hipMemcpyHostToDevice, st) !=
+        hipSuccess)
+      return false;
+  }
+  lora_demod_outputs o{};
+  o.symbols = reinterpret_cast<uint16_t*>(dev + d.syms);
+  o.sym_stride = std::max<int64_t>(nsym, 1);
+  o.sync = dev + d.sync;
+  o.cfo = reinterpret_cast<float*>(dev + d.cfo);
+  o.time_offset = reinterpret_cast<float*>(dev + d.toff);
+  o.max_amp = reinterpret_cast<float*>(dev + d.maxa);
+  if (lora_demod_batch(g.plan, reinterpret_cast<const float*>(dev + d.iq), 1, (int64_t)count, (int64_t)count, &o,
+                       dev + d.ws, d.total - d.ws, st) < 0)
+    return false;
+  // symbols, then the four per-frame outputs (256-byte slots, contiguous): two copies
+  if ((nsym > 0 && hipMemcpyAsync(host + d.syms, dev + d.syms, (size_t)nsym * sizeof(uint16_t),
+                                  hipMemcpyDeviceToHost, st) != hipSuccess) ||
+      hipMemcpyAsync(host + d.sync, dev + d.sync, d.ws - d.sync, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return false;
+  out.nsym = nsym;
+  out.sync = host[d.sync];
+  std::memcpy(&out.cfo, host + d.cfo, 4);
+  std::memcpy(&out.toff, host + d.toff, 4);
+  std::memcpy(&out.max_amp, host + d.maxa, 4);
+  out.syms = reinterpret_cast<const uint16_t*>(host + d.syms);
+  return true;
+}
+
+int window_code(lora_phy::window_type w) {
+  return w == lora_phy::window_type::window_hann ? LORA_WINDOW_HANN : LORA_WINDOW_NONE;
 }
 
 }  // namespace
 
 namespace lora_phy {
 
+void detail::release(device_state& g) {
+  if (g.stream) hipStreamSynchronize(static_cast<hipStream_t>(g.stream));
+  if (g.dev) hipFree(g.dev);
+  if (g.host) hipHostFree(g.host);
+  if (g.plan) lora_demod_plan_destroy(g.plan);
+  if (g.stream) hipStreamDestroy(static_cast<hipStream_t>(g.stream));
+  g = device_state{};
+}
+
+// ---------------------------------------------------------------------------------------
+// Legacy helpers (phy.hpp:158-215)
+// ---------------------------------------------------------------------------------------
+
 void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win, std::complex<float>* scratch,
                      size_t max_samples) {
   if (!ws) return;
+  // the reference's init overwrites every field: a workspace initialised before (for any
+  // sf / window) gives up its device resources first
+  detail::release(ws->gpu);
   ws->N = size_t(1) << sf;
-  ws->sf = sf;
   ws->window_kind = win;
   ws->scratch = scratch;
   ws->scratch_len = max_samples;
   ws->metrics = lora_metrics{};
   int dev = 0;
   hipGetDevice(&dev);
-  ws->device = dev;
-  hipStream_t st = nullptr;
-  if (!ws->stream && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) ws->stream = st;
-  // device resources for the common case (osr 1, max_samples), so that lora_demodulate
-  // allocates nothing (no_alloc_test.cpp:78-99)
-  if (ensure_plan(ws, 1) && max_samples > 0) ensure_dev(ws, max_samples);
+  ws->gpu.device = dev;
+  if (sf < 2 || sf > 12 || !ensure_stream(ws->gpu)) return;
+  // Device resources for osr 1 and frames of max_samples, then one warm-up call per
+  // kernel family (the runtime loads code objects and sets up the stream on first use),
+  // so that lora_demodulate on such a frame allocates nothing (no_alloc_test.cpp:78-99).
+  if (!ensure_plan(ws->gpu, sf, 1, window_code(win), 125000, LORA_MODE_LEGACY)) return;
+  const size_t n = std::max<size_t>(max_samples, 3 * ws->N);
+  if (!ensure_buffers(ws->gpu, n)) return;
+  const DevLayout d = layout(ws->gpu.plan, ws->gpu.samples, ws->N);
+  std::complex<float>* zeros = reinterpret_cast<std::complex<float>*>(static_cast<unsigned char*>(ws->gpu.host) + d.iq);
+  std::memset(zeros, 0, n * sizeof(std::complex<float>));
+  FrameOut o;
+  run_frame(ws->gpu, zeros, n, o);      // speculative pipeline (3+ symbols)
+  run_frame(ws->gpu, zeros, ws->N, o);  // one symbol: three-launch path
 }
 
 void lora_demod_free(lora_demod_workspace* ws) {
   if (!ws) return;
-  if (ws->stream) hipStreamSynchronize(static_cast<hipStream_t>(ws->stream));
-  if (ws->dev) hipFree(ws->dev);
-  if (ws->plan) lora_demod_plan_destroy(ws->plan);
-  if (ws->stream) hipStreamDestroy(static_cast<hipStream_t>(ws->stream));
-  ws->dev = nullptr;
-  ws->dev_samples = 0;
-  ws->plan = nullptr;
-  ws->plan_osr = 0;
-  ws->stream = nullptr;
+  detail::release(ws->gpu);
   ws->N = 0;
   ws->scratch = nullptr;
   ws->scratch_len = 0;
@@ -144,67 +261,51 @@ size_t lora_demodulate(lora_demod_workspace* ws, const std::complex<float>* samp
                        uint16_t* out_symbols, unsigned osr, uint8_t* out_sync) {
   if (!ws || ws->N == 0 || !samples) return 0;
   if (osr == 0) osr = 1;
-  if (!ensure_plan(ws, osr) || !ensure_dev(ws, std::max<size_t>(sample_count, 1))) return 0;
-  hipStream_t st = static_cast<hipStream_t>(ws->stream);
-  const DevLayout d = layout(ws->plan, ws->dev_samples, ws->N);
-  unsigned char* base = static_cast<unsigned char*>(ws->dev);
-  const int64_t nsym = lora_demod_symbols_per_frame(ws->plan, (int64_t)sample_count);
-  if (nsym < 0) return 0;
-  if (sample_count > 0 &&
-      hipMemcpyAsync(base + d.iq, samples, sample_count * sizeof(std::complex<float>), hipMemcpyHostToDevice,
-                     st) != hipSuccess)
+  unsigned sf = 0;
+  while ((size_t(1) << sf) < ws->N) ++sf;
+  if (!ensure_stream(ws->gpu) ||
+      !ensure_plan(ws->gpu, sf, osr, window_code(ws->window_kind), 125000, LORA_MODE_LEGACY) ||
+      !ensure_buffers(ws->gpu, std::max<size_t>(sample_count, 1)))
     return 0;
-  lora_demod_outputs o{};
-  o.symbols = reinterpret_cast<uint16_t*>(base + d.syms);
-  o.sym_stride = std::max<int64_t>(nsym, 1);
-  o.sync = base + d.sync;
-  o.cfo = reinterpret_cast<float*>(base + d.cfo);
-  o.time_offset = reinterpret_cast<float*>(base + d.toff);
-  o.max_amp = reinterpret_cast<float*>(base + d.maxa);
-  if (lora_demod_batch(ws->plan, reinterpret_cast<const float*>(base + d.iq), 1, (int64_t)sample_count,
-                       (int64_t)sample_count, &o, base + d.ws, d.total - d.ws, st) < 0)
-    return 0;
-  uint8_t sync = 0;
-  float cfo = 0.0f, toff = 0.0f, maxa = 0.0f;
-  if (hipMemcpyAsync(&sync, o.sync, 1, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(&cfo, o.cfo, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(&toff, o.time_offset, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(&maxa, o.max_amp, 4, hipMemcpyDeviceToHost, st) != hipSuccess)
-    return 0;
-  if (nsym > 0 && out_symbols &&
-      hipMemcpyAsync(out_symbols, o.symbols, (size_t)nsym * sizeof(uint16_t), hipMemcpyDeviceToHost, st) !=
-          hipSuccess)
-    return 0;
-  if (hipStreamSynchronize(st) != hipSuccess) return 0;
+  FrameOut o;
+  if (!run_frame(ws->gpu, samples, sample_count, o)) return 0;
   // LoRaDemod.cpp:68-71: a frame that needs rescaling without a large enough scratch
-  // buffer returns 0 before anything is written (the symbols were copied above; the
-  // caller's buffer content is unspecified then, as with a partially written output).
-  if (maxa > 1.0f && (!ws->scratch || ws->scratch_len < sample_count)) return 0;
-  ws->metrics.cfo = cfo;
-  ws->metrics.time_offset = toff;
-  if (out_sync) *out_sync = sync;
-  return (size_t)nsym;
+  // buffer returns 0 before anything is written
+  if (o.max_amp > 1.0f && (!ws->scratch || ws->scratch_len < sample_count)) return 0;
+  if (o.nsym > 0 && out_symbols) std::memcpy(out_symbols, o.syms, (size_t)o.nsym * sizeof(uint16_t));
+  ws->metrics.cfo = o.cfo;
+  ws->metrics.time_offset = o.toff;
+  if (out_sync) *out_sync = o.sync;
+  return (size_t)o.nsym;
 }
 
 size_t lora_modulate(const uint16_t* symbols, size_t symbol_count, std::complex<float>* out_samples, unsigned sf,
                      unsigned osr, bandwidth bw, float amplitude, uint8_t sync) {
   if (osr == 0) osr = 1;
+  if (sf < 2 || sf > 12) return 0;
   const size_t per = (symbol_count + 2) * (size_t(1) << sf) * osr;
   if (!out_samples || (symbol_count > 0 && !symbols)) return 0;
-  // per-thread device staging, grown on demand (the reference's lora_modulate takes no
-  // workspace)
+  // per-thread device staging, grown on demand and tied to the device it was allocated
+  // on (the reference's lora_modulate takes no workspace)
   thread_local void* dev = nullptr;
   thread_local size_t cap = 0;
+  thread_local int dev_id = -1;
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return 0;
   const size_t need = align256(per * 8) + align256(symbol_count * 2 + 2);
-  if (cap < need) {
-    if (dev) hipFree(dev);
+  if (cap < need || dev_id != device) {
+    if (dev) {
+      hipSetDevice(dev_id);
+      hipFree(dev);
+      hipSetDevice(device);
+    }
     dev = nullptr;
     cap = 0;
+    dev_id = -1;
     if (hipMalloc(&dev, need) != hipSuccess) return 0;
     cap = need;
+    dev_id = device;
   }
-  int device = 0;
-  hipGetDevice(&device);
   float* iq = static_cast<float*>(dev);
   uint16_t* s = reinterpret_cast<uint16_t*>(static_cast<unsigned char*>(dev) + align256(per * 8));
   if (symbol_count > 0 && hipMemcpy(s, symbols, symbol_count * 2, hipMemcpyHostToDevice) != hipSuccess) return 0;
@@ -229,6 +330,154 @@ size_t lora_decode(const uint16_t* symbols, size_t symbol_count, uint8_t* out_by
   for (size_t i = 0; i + 1 < symbol_count; i += 2)
     out_bytes[k++] = (uint8_t)((dec_h84_nibble((uint8_t)symbols[i]) << 4) | dec_h84_nibble((uint8_t)symbols[i + 1]));
   return k;
+}
+
+// ---------------------------------------------------------------------------------------
+// Workspace API (phy.hpp:96-156, phy.cpp:26-261)
+// ---------------------------------------------------------------------------------------
+
+int init(lora_workspace* ws, const lora_params* cfg) {
+  if (!ws || !cfg) return -1;                  // phy.cpp:27
+  if (cfg->sf < 2 || cfg->sf > 12) return -1;  // kissfft's static plans hold N <= 4096 (kissfft.hh:34)
+  const unsigned bw_hz = static_cast<unsigned>(cfg->bw);
+  if (bw_hz != 125000 && bw_hz != 250000 && bw_hz != 500000) return -1;
+  const int N = 1 << cfg->sf;
+  ws->metrics = {};
+  ws->osr = cfg->osr ? cfg->osr : 1u;
+  ws->bw = cfg->bw;
+  ws->sync_word = cfg->sync_word;
+  ws->window_kind = cfg->window;
+  if (ws->window) {  // phy.cpp:36-47, into the caller's window buffer
+    for (int i = 0; i < N; ++i)
+      ws->window[i] = ws->window_kind == window_type::window_hann
+                          ? 0.5f - 0.5f * std::cos(2.0f * float(M_PI) * static_cast<float>(i) /
+                                                   (static_cast<float>(N) - 1.0f))
+                          : 1.0f;
+  }
+  // device side: an API-mode plan (raw-sample estimate, per-symbol down-chirp,
+  // phy.cpp:178-239) for this sf / osr / bandwidth / window
+  detail::release(ws->gpu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  ws->gpu.device = dev;
+  // phy.cpp:97,223: the window applies only when the caller supplied the buffer
+  const window_type eff = ws->window ? cfg->window : window_type::window_none;
+  if (!ensure_stream(ws->gpu) || !ensure_plan(ws->gpu, cfg->sf, ws->osr, window_code(eff), bw_hz, LORA_MODE_API))
+    return -1;
+  return 0;
+}
+
+void reset(lora_workspace* ws) {
+  if (ws) ws->metrics = {};
+}
+
+ssize_t encode(lora_workspace* ws, const uint8_t* payload, size_t payload_len, uint16_t* symbols,
+               size_t symbol_cap) {
+  if (!ws || !payload || !symbols) return -1;
+  if (2 * payload_len > symbol_cap) return -1;  // phy.cpp:60 (checked before writing here)
+  return static_cast<ssize_t>(lora_encode(payload, payload_len, symbols, ws->gpu.sf));
+}
+
+ssize_t decode(lora_workspace* ws, const uint16_t* symbols, size_t symbol_count, uint8_t* payload,
+               size_t payload_cap) {
+  if (!ws || !symbols || !payload) return -1;
+  if (symbol_count / 2 > payload_cap) return -1;  // phy.cpp:245 (checked before writing here)
+  const size_t produced = lora_decode(symbols, symbol_count, payload);
+  if (produced >= 4) {  // phy.cpp:247-254: SX1272 CRC over payload[2 .. produced - 2)
+    const size_t data_len = produced - 4;
+    const uint16_t provided = (uint16_t)(payload[produced - 2] | (payload[produced - 1] << 8));
+    ws->metrics.crc_ok = provided == sx1272_data_checksum(payload + 2, (int)data_len);
+  } else {
+    ws->metrics.crc_ok = false;
+  }
+  return static_cast<ssize_t>(produced);
+}
+
+ssize_t modulate(lora_workspace* ws, const uint16_t* symbols, size_t symbol_count, std::complex<float>* iq,
+                 size_t iq_cap) {
+  if (!ws || !symbols || !iq || !ws->gpu.plan) return -1;
+  const unsigned sf = ws->gpu.sf, osr = ws->osr ? ws->osr : 1u;
+  if ((symbol_count + 2) * (size_t(1) << sf) * osr > iq_cap) return -1;  // phy.cpp:74 (before writing here)
+  const size_t produced = lora_modulate(symbols, symbol_count, iq, sf, osr, ws->bw, 1.0f, ws->sync_word);
+  return produced ? static_cast<ssize_t>(produced) : -1;
+}
+
+ssize_t demodulate(lora_workspace* ws, const std::complex<float>* iq, size_t sample_count, uint16_t* symbols,
+                   size_t symbol_cap) {
+  if (!ws || !iq || !symbols || !ws->gpu.plan) return -1;  // phy.cpp:181
+  const size_t N = size_t(1) << ws->gpu.sf;
+  const size_t step = N * (ws->osr ? ws->osr : 1u);
+  if (sample_count % step != 0) return -1;  // phy.cpp:186
+  const size_t total = sample_count / step;
+  if (total < 2) return -1;               // phy.cpp:188
+  if (total - 2 > symbol_cap) return -1;  // phy.cpp:190
+  if (!ensure_buffers(ws->gpu, sample_count)) return -1;
+  FrameOut o;
+  if (!run_frame(ws->gpu, iq, sample_count, o)) return -1;
+  std::memcpy(symbols, o.syms, (size_t)o.nsym * sizeof(uint16_t));
+  ws->metrics.cfo = o.cfo;  // estimate_offsets on the first two symbols (phy.cpp:192-193)
+  ws->metrics.time_offset = o.toff;
+  ws->sync_word = o.sync;  // phy.cpp:235-237
+  return static_cast<ssize_t>(o.nsym);
+}
+
+void estimate_offsets(lora_workspace* ws, const std::complex<float>* samples, size_t sample_count) {
+  if (!ws || !samples || sample_count == 0 || !ws->gpu.plan) return;  // phy.cpp:81
+  detail::device_state& g = ws->gpu;
+  if (!ensure_buffers(g, sample_count)) return;
+  hipStream_t st = static_cast<hipStream_t>(g.stream);
+  const DevLayout d = layout(g.plan, g.samples, size_t(1) << g.sf);
+  unsigned char* dev = static_cast<unsigned char*>(g.dev);
+  unsigned char* host = static_cast<unsigned char*>(g.host);
+  std::memcpy(host + d.iq, samples, sample_count * sizeof(std::complex<float>));
+  std::memcpy(host + d.cfo, &ws->metrics.cfo, 4);  // left untouched when no whole symbol (phy.cpp:87)
+  std::memcpy(host + d.toff, &ws->metrics.time_offset, 4);
+  if (hipMemcpyAsync(dev + d.iq, host + d.iq, sample_count * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dev + d.cfo, host + d.cfo, 256 * 2, hipMemcpyHostToDevice, st) != hipSuccess)
+    return;
+  if (lora_estimate_offsets_batch(g.plan, reinterpret_cast<const float*>(dev + d.iq), 1, (int64_t)sample_count,
+                                  (int64_t)sample_count, reinterpret_cast<float*>(dev + d.cfo),
+                                  reinterpret_cast<float*>(dev + d.toff), st) < 0)
+    return;
+  if (hipMemcpyAsync(host + d.cfo, dev + d.cfo, 256 * 2, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return;
+  std::memcpy(&ws->metrics.cfo, host + d.cfo, 4);
+  std::memcpy(&ws->metrics.time_offset, host + d.toff, 4);
+}
+
+void compensate_offsets(const lora_workspace* ws, std::complex<float>* samples, size_t sample_count) {
+  if (!ws || !samples || sample_count == 0 || !ws->gpu.plan) return;  // phy.cpp:150
+  // the device state is this call's scratch (the reference's signature takes a const
+  // workspace and only reads its metrics)
+  detail::device_state& g = const_cast<detail::device_state&>(ws->gpu);
+  if (!ensure_buffers(g, 2 * sample_count)) return;  // in and out, out of place
+  hipStream_t st = static_cast<hipStream_t>(g.stream);
+  const DevLayout d = layout(g.plan, g.samples, size_t(1) << g.sf);
+  unsigned char* dev = static_cast<unsigned char*>(g.dev);
+  unsigned char* host = static_cast<unsigned char*>(g.host);
+  float* io = reinterpret_cast<float*>(host + d.iq);
+  std::memcpy(io, samples, sample_count * 8);
+  std::memcpy(host + d.cfo, &ws->metrics.cfo, 4);
+  std::memcpy(host + d.toff, &ws->metrics.time_offset, 4);
+  float* din = reinterpret_cast<float*>(dev + d.iq);
+  float* dout = din + 2 * sample_count;
+  if (hipMemcpyAsync(din, io, sample_count * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(dev + d.cfo, host + d.cfo, 256 * 2, hipMemcpyHostToDevice, st) != hipSuccess)
+    return;
+  if (lora_compensate_offsets_batch(g.sf, ws->osr ? ws->osr : 1u, din, 1, (int64_t)sample_count,
+                                    (int64_t)sample_count, reinterpret_cast<const float*>(dev + d.cfo),
+                                    reinterpret_cast<const float*>(dev + d.toff), g.device, st, dout) < 0)
+    return;
+  if (hipMemcpyAsync(io, dout, sample_count * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return;
+  std::memcpy(samples, io, sample_count * 8);
+}
+
+const lora_metrics* get_last_metrics(const lora_workspace* ws) {
+  if (!ws) return nullptr;
+  return &ws->metrics;
 }
 
 }  // namespace lora_phy

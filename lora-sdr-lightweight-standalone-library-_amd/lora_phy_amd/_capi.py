@@ -99,7 +99,7 @@ def lib() -> C.CDLL:
     L.lora_demod_symbols_per_frame.restype = C.c_int64
     L.lora_demod_symbols_per_frame.argtypes = [C.c_void_p, C.c_int64]
     L.lora_demod_workspace_bytes.restype = C.c_size_t
-    L.lora_demod_workspace_bytes.argtypes = [C.c_void_p, C.c_int64]
+    L.lora_demod_workspace_bytes.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
     L.lora_demod_batch.restype = C.c_int64
     L.lora_demod_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
                                    C.POINTER(DemodOutputs), C.c_void_p, C.c_size_t, C.c_void_p]

@@ -127,8 +127,8 @@ class DemodPlan:
         certification margin was too small); synchronises the device."""
         return _capi.check(self._lib.lora_demod_spec_recomputed(self._h))
 
-    def _workspace(self, frames: int) -> torch.Tensor:
-        need = self._lib.lora_demod_workspace_bytes(self._h, int(frames))
+    def _workspace(self, frames: int, frame_len: int) -> torch.Tensor:
+        need = self._lib.lora_demod_workspace_bytes(self._h, int(frames), int(frame_len))
         key = _stream_handle(self.device)
         ws = self._ws.get(key)
         if ws is None or ws.numel() < need:
@@ -162,7 +162,7 @@ class DemodPlan:
             for name, dt in (("sync", torch.uint8), ("cfo", torch.float32), ("time_offset", torch.float32),
                              ("max_amp", torch.float32)):
                 _check_buf(getattr(out, name), "out." + name, dt, dev, F)
-        ws = self._workspace(F)
+        ws = self._workspace(F, L)
         o = _capi.DemodOutputs(out.symbols.data_ptr() if S > 0 else None,
                                out.symbols.stride(0) if S > 0 else 0,
                                out.sync.data_ptr(), out.cfo.data_ptr(), out.time_offset.data_ptr(),

@@ -26,7 +26,7 @@ def test_batch_error_codes(amd):
     F, L = 4, 66 * 128
     iq = torch.zeros((F, L), dtype=torch.complex64, device="cuda")
     syms = torch.zeros((F, 64), dtype=torch.uint16, device="cuda")
-    ws = torch.zeros(lib.lora_demod_workspace_bytes(plan._h, F), dtype=torch.uint8, device="cuda")
+    ws = torch.zeros(lib.lora_demod_workspace_bytes(plan._h, F, L), dtype=torch.uint8, device="cuda")
     out = _capi.DemodOutputs(syms.data_ptr(), 64, None, None, None, None)
     ok = lib.lora_demod_batch(plan._h, iq.data_ptr(), F, L, L, C.byref(out), ws.data_ptr(), ws.numel(), None)
     assert ok == 64

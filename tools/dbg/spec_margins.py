@@ -28,7 +28,7 @@ print("recomputed", plan.spec_recomputed(), "kernels", plan.last_kernels())
 ws = next(iter(plan._ws.values())).cpu().numpy()
 def al(b):
     return (b + 255) & ~255
-cnt = al(F * 80 * 4)  # ws_counter_bytes: frames * kMaxBpf u32 (check lora_capi.hip)
+cnt = al(F * max(1, min(80, S * N // 4096)) * 4)  # ws_layout: frames * frame_max_blocks u32 (lora_capi.hip)
 par = al(F * 32)
 fp = ws[cnt:cnt + F * 32].view(np.float32).reshape(F, 8)
 fps = ws[cnt + par:cnt + par + F * 32].view(np.float32).reshape(F, 8)
