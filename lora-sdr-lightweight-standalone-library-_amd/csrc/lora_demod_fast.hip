@@ -265,7 +265,8 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
 #pragma unroll
       for (int gg = 0; gg < NG; ++gg) {
         const cf v = x[gg * R + u];
-        const float m2 = v.re * v.re + v.im * v.im;
+        // FMA (certified demod): |X|^2 with one rounding fewer, inside the bound's E
+        const float m2 = FMA ? __builtin_fmaf(v.re, v.re, v.im * v.im) : v.re * v.re + v.im * v.im;
         const uint32_t bin = (uint32_t)(l + T * gg + MA * u);
         // runner-up |X|^2 of the lane (an equal value counts: margin 0); sec <= best, so
         // the median of (sec, m2, best) is best if m2 > best, else max(sec, m2)
@@ -664,6 +665,7 @@ constexpr int demod_twl_entries() {
   }
 }
 
+
 // SPEC: the speculative single-read pipeline's symbol pass (lora_capi.hip): the pre-pass
 // offsets (fp_spec) on unscaled samples, and per data symbol (spec_marg, one 8-byte
 // store) the margin |X1| - |X2| between the top bin and the runner-up and the window's
@@ -688,11 +690,17 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
 
   const int g = tid / T;  // slot
   const int l = tid % T;  // lane within the symbol
-  const int64_t w = (int64_t)blockIdx.x * SPW + g;
+  // work item w -> (frame f, symbol s): one 64-bit division per workgroup on the scalar
+  // unit, then a small per-lane quotient (the SPW symbols of a workgroup span few frames)
+  const int64_t w0 = (int64_t)blockIdx.x * SPW;
+  const int64_t f0 = w0 / per;
+  const int r0 = (int)(w0 - f0 * per);
+  const int64_t w = w0 + g;
   const bool valid = w < work;
-  const int64_t wc = valid ? w : work - 1;  // clamp: invalid lanes mirror a valid symbol
-  const int64_t f = wc / per;
-  const int s = s0 + (int)(wc - f * per);
+  const int loc = r0 + (int)((valid ? w : work - 1) - w0);  // clamp: invalid lanes mirror a valid symbol
+  const int q = per >= SPW ? (loc >= per ? 1 : 0) : (int)((unsigned)loc / (unsigned)per);
+  const int64_t f = f0 + q;
+  const int s = s0 + (loc - q * per);
   const FrameParams p = RAW ? FrameParams{0.0f, 0.0f, 0.0f, 1.0f, 0, 0, 0, 0} : (SPEC ? a.fp_spec[f] : a.fp[f]);
   int64_t base;
   int cg;
@@ -748,6 +756,174 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   }
 }
 
+// Diagnostic build only (tools/build_variant.sh stamps -DLORA_STAMPS; never in the
+// product library): per wave of the speculative demod, the shader clock at the end of
+// each phase and the 100 MHz real-time clock at start and end, into a buffer of its own
+// that no code reads (lora_debug_stamps copies it out).  tools/stamps.py reads it.
+#ifdef LORA_STAMPS
+constexpr int kStampWaves = 1 << 17;
+__device__ unsigned long long g_stamps[kStampWaves * 8];
+__device__ unsigned long long g_stamps_est[3][kStampWaves * 8];  // [SPEC stage 0/1/2]
+__device__ __forceinline__ void stamp_to(unsigned long long* buf, int k, bool real) {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  if (real)
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  else
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && wv < (unsigned)kStampWaves) buf[(size_t)wv * 8 + k] = t;
+}
+#define LORA_ESTAMP(k, real) stamp_to(g_stamps_est[SPEC], k, real)
+__device__ __forceinline__ void stamp(int k, bool real) {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  if (real)
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  else
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && wv < (unsigned)kStampWaves) g_stamps[(size_t)wv * 8 + k] = t;
+}
+#define LORA_STAMP(k, real) \
+  if (r == 0) stamp(k, real)
+#else
+#define LORA_STAMP(k, real)
+#define LORA_ESTAMP(k, real)
+#endif
+
+// ---- the speculative pipeline's symbol pass -----------------------------------------
+// k_spec_demod: every data symbol of LEGACY osr-1 unwindowed frames (MODE 0: fused caller
+// dechirp from the paired table KArgs::downP; MODE 1: dechirped input) with the pre-pass
+// offsets (fp_spec) on UNSCALED samples, the hardware rotation and fused multiply-adds,
+// the symbol's index, its top-bin / runner-up margin and its window's max(|I|,|Q|) (one
+// 8-byte spec_marg store), certified or recomputed exactly by k_est_fast<SPEC = 2>.  The
+// arithmetic is k_demod_fast<SF, MODE, true, true>'s.  A workgroup runs ROUNDS groups of
+// SPW symbols; the samples and table values of round r + 1 are requested as soon as
+// round r's have been dechirped (their registers are free again), so they are in flight
+// during round r's transform and reductions.
+#ifndef LORA_SPEC_ROUNDS
+#define LORA_SPEC_ROUNDS 1
+#endif
+#ifndef LORA_SPEC_PF_TAB
+#define LORA_SPEC_PF_TAB 1  // ROUNDS > 1: prefetch the next round's table pairs too (else at its start)
+#endif
+template <int SF, int MODE, int ROUNDS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
+LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t work, int rowc) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
+  constexpr bool WL = G::WAVE_LOCAL;
+  constexpr int NTW = demod_twl_entries<SF, true>();
+  static_assert(P == 16 && (MODE == 0 || MODE == 1), "SF >= 6, LEGACY osr 1");
+  static_assert(NTW <= 256, "one staged twiddle per thread");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint64_t red[4];
+  cf* rows = reinterpret_cast<cf*>(smem);
+  cf* twl = rows + (size_t)SPW * rowc;
+  const int tid = threadIdx.x;
+  const int per = a.total - 2;
+  const int g = tid / T;  // slot
+  const int l = tid % T;  // lane within the symbol
+  cf tv{0.0f, 0.0f};
+  if constexpr (NTW > 0) {  // issued first: it returns ahead of the symbol's gathers
+    if (tid < NTW) tv = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
+  }
+  // work item -> (frame, data symbol j): one 64-bit division per workgroup (scalar unit),
+  // then small per-lane quotients
+  const int64_t wb = (int64_t)blockIdx.x * (SPW * ROUNDS);
+  const int64_t fb = wb / per;
+  const int rb = (int)(wb - fb * per);
+  int64_t fr[ROUNDS];
+  int jr[ROUNDS];
+  bool vr[ROUNDS];
+  float rate[ROUNDS];
+  int toff[ROUNDS];
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    const int64_t w = wb + r * SPW + g;
+    vr[r] = w < work;
+    const int loc = rb + (int)((vr[r] ? w : work - 1) - wb);  // invalid lanes mirror a valid symbol
+    const int q = per >= SPW * ROUNDS ? (loc >= per ? 1 : 0) : (int)((unsigned)loc / (unsigned)per);
+    fr[r] = fb + q;
+    jr[r] = loc - q * per;
+    const FrameParams& fp = a.fp_spec[fr[r]];  // rate and t_off of every round, requested up front
+    rate[r] = fp.rate;
+    toff[r] = fp.t_off;
+  }
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  cf in[P];
+  float4 dt[P / 2];
+  auto request = [&](int r, bool iq, bool tab) {  // round r's samples (read once: nontemporal), table pairs
+    const int s = 2 + jr[r];
+    int64_t base;
+    int cg;
+    sym_base(s, N, a.frame_len, toff[r], base, cg);
+    if (iq) {
+      const v2f* __restrict__ xl = reinterpret_cast<const v2f*>(a.iq + fr[r] * a.frame_stride + base + l);
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const v2f v = __builtin_nontemporal_load(xl + T * q);
+        in[q] = cf{v.x, v.y};
+      }
+    }
+    if constexpr (MODE == 0) {
+      if (tab) {
+        const float4* __restrict__ dp = reinterpret_cast<const float4*>(a.downP) + cg + l;
+#pragma unroll
+        for (int pp = 0; pp < P / 2; ++pp) dt[pp] = dp[pp * (N + T)];
+      }
+    }
+  };
+  request(0, true, true);
+  if constexpr (NTW > 0) {
+    if (tid < NTW) twl[tid] = tv;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    LORA_STAMP(5, true);
+    LORA_STAMP(0, false);
+    if (r > 0 && !LORA_SPEC_PF_TAB) request(r, false, true);
+    // caller-side dechirp (e2e_chain_test.cpp:88-93) with the reference's products, the
+    // window's max(|I|,|Q|) of exactly these samples, then the rotation
+    if constexpr (MODE == 0) {
+#pragma unroll
+      for (int pp = 0; pp < P / 2; ++pp) {
+        in[2 * pp] = cmul(in[2 * pp], cf{dt[pp].x, dt[pp].y});
+        in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
+      }
+    }
+    float pm = 0.0f;
+#pragma unroll
+    for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
+    LORA_STAMP(1, false);
+    const int s = 2 + jr[r];
+    const float start = rate[r] * ((float)((uint32_t)s * (uint32_t)N) + (float)toff[r]);
+    cf z[P];
+    rotate_place<SF, true, true, true>(in, z, start, rate[r], false, a.win, l);
+    asm volatile("" : "+v"(pm));
+    LORA_STAMP(2, false);
+    if (r + 1 < ROUNDS) request(r + 1, true, LORA_SPEC_PF_TAB);  // into the registers the dechirp just freed
+    float sec = 0.0f;
+    const uint64_t lkey = fft_key<SF, false, true, (NTW > 0)>(z, rows + (size_t)g * rowc, l, a, &sec, twl);
+    LORA_STAMP(3, false);
+    const uint64_t key = symbol_key<SF>(lkey, tid, red);
+    // runner-up over the symbol: the top lane offers its own runner-up, the others their best
+    float r2 = lkey == key ? sec : key_value(lkey);
+    group_reduce2<SF>(r2, pm, tid, reinterpret_cast<float*>(smem + 64));
+    if (l == 0 && vr[r]) {
+      if (a.syms) a.syms[fr[r] * a.sym_stride + jr[r]] = (uint16_t)key_index(key);
+      reinterpret_cast<float2*>(a.spec_marg)[fr[r] * per + jr[r]] = make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm);
+    }
+    LORA_STAMP(4, false);
+    LORA_STAMP(6, true);
+    if (r + 1 < ROUNDS) block_sync<WL>();  // the rows (and group_reduce2's scratch) are rewritten next round
+  }
+}
+
 // Offset estimate + sync symbols, one T-lane group per frame (LoRaDemod.cpp:79-135,
 // 165-168, 177-192; phy.cpp:78-145, 228-237), for frames with >= 2 whole symbols.
 // Per frame: for each of symbols 0,1 and osr phase t, the FFT of the (dechirped,
@@ -794,6 +970,8 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   // (frames of up to kSpecChunks * T data symbols)
   __shared__ unsigned long long fmask[SPEC == 2 ? SPB : 1][SPEC == 2 ? T : 1];
   const int tid = threadIdx.x;
+  LORA_ESTAMP(5, true);
+  LORA_ESTAMP(0, false);
   const int step = DYN ? a.step : N;
   const int osr = DYN ? a.osr : 1;
   const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
@@ -825,6 +1003,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   }
   const int scaled = maxv > 1.0f;
   const float scale = scaled ? 1.0f / maxv : 1.0f;
+  LORA_ESTAMP(1, false);
   if constexpr (SPEC == 2) {
     // max <= 1: no rescaling, so the pre-pass estimate and its sync word are already the
     // reference's (identical inputs and arithmetic); the symbols, rotated with the
@@ -973,6 +1152,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         have_prev = true;
       }
     }
+    LORA_ESTAMP(2, false);
     if (l == 0) {
       const float avg_index = sum_index / 2.0f;
       const float cfo_coarse = avg_index / (float)N;
@@ -1003,6 +1183,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     }
     block_sync<G::WAVE_LOCAL>();
     q = sp[g];
+    LORA_ESTAMP(3, false);
     if constexpr (SPEC == 1) {
       // The samples outside every data-symbol window of the pre-pass offsets: [0, start of
       // symbol 2's window) and [end of the last window, frame_len).  With the windows'
@@ -1031,7 +1212,11 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       if (l == 0 && valid) a.spec_max[f] = (uint32_t)(mk >> 32);
       // Already above 1: the frame is rescaled, so k_est_fast<SPEC = 2> recomputes the
       // estimate and the sync word; skip them here (frame-uniform exit).
-      if (__uint_as_float((uint32_t)(mk >> 32)) > 1.0f) return;
+      if (__uint_as_float((uint32_t)(mk >> 32)) > 1.0f) {
+        LORA_ESTAMP(4, false);
+        LORA_ESTAMP(6, true);
+        return;
+      }
       block_sync<G::WAVE_LOCAL>();  // red is reused by the sync symbols
     }
     uint32_t sw[2];
@@ -1076,7 +1261,11 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         a.sync[f] = word;
       }
     }
-    if constexpr (SPEC == 1) return;
+    LORA_ESTAMP(4, false);
+    if constexpr (SPEC == 1) {
+      LORA_ESTAMP(6, true);
+      return;
+    }
   }  // exact estimate
   if constexpr (SPEC == 2) {
     // ---- certification of the data symbols the demod computed speculatively ----
@@ -1133,6 +1322,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       }
     }
     block_sync<G::WAVE_LOCAL>();
+    LORA_ESTAMP(7, false);
     cf in[P], z[P];
     for (int w = 0; w < (per + 63) >> 6; ++w) {  // group-uniform: every lane reads the same words
       unsigned long long m = fmask[g][w];
@@ -1155,6 +1345,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         block_sync<G::WAVE_LOCAL>();  // row is rewritten by the next transform
       }
     }
+    LORA_ESTAMP(6, true);
   }
 }
 
@@ -1205,6 +1396,22 @@ bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   return true;
 }
 
+template <int SF, int MODE>
+bool launch_spec_demod(const KArgs& a, int64_t work, hipStream_t st) {
+  using G = Geo<SF>;
+  constexpr int R = LORA_SPEC_ROUNDS;
+  const int rowc = row_complex<SF>();
+  const size_t lds = sizeof(cf) * ((size_t)G::SPW * rowc + demod_twl_entries<SF, true>());
+  if (lds > 160 * 1024) return false;
+  if (lds > 64 * 1024)
+    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return false;
+  const int64_t grid = (work + G::SPW * R - 1) / (G::SPW * R);
+  hipLaunchKernelGGL((k_spec_demod<SF, MODE, R>), dim3((unsigned)grid), dim3(256), lds, st, a, work, rowc);
+  return true;
+}
+
 // The speculative pipeline's three launches for SF 6-12, MODE 0/1 (see lora_capi.hip).
 template <int SF>
 bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
@@ -1214,7 +1421,7 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
     const int64_t work = frames * (int64_t)(a.total - 2);
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
     if (stage == 1)
-      return a.dechirp ? launch_mode<SF, 0, true, true>(a, 2, work, st) : launch_mode<SF, 1, true, true>(a, 2, work, st);
+      return a.dechirp ? launch_spec_demod<SF, 0>(a, work, st) : launch_spec_demod<SF, 1>(a, work, st);
     return a.dechirp ? launch_est_mode<SF, 0, 2>(a, frames, st) : launch_est_mode<SF, 1, 2>(a, frames, st);
   }
 }
@@ -1234,6 +1441,22 @@ bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
 }
 
 }  // namespace
+
+#ifdef LORA_STAMPS
+extern "C" int lora_debug_stamps(unsigned long long* host, size_t n) {
+  n = n < (size_t)kStampWaves * 8 ? n : (size_t)kStampWaves * 8;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -5;
+}
+// stage 0 / 1 / 2 of the estimate kernels (k_est_fast<SF, MODE, SPEC = stage>)
+extern "C" int lora_debug_stamps_est(int stage, unsigned long long* host, size_t n) {
+  n = n < (size_t)kStampWaves * 8 ? n : (size_t)kStampWaves * 8;
+  if (stage < 0 || stage > 2) return -22;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_est), n * sizeof(unsigned long long),
+                             (size_t)stage * kStampWaves * 8 * sizeof(unsigned long long)) == hipSuccess
+             ? 0
+             : -5;
+}
+#endif
 
 bool launch_spec(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   switch (a.sf) {

@@ -4,7 +4,9 @@ LoRa frames (and channels) are independent: rank r demodulates a
 contiguous block of frames on its own GPU.  Collectives appear only around the
 measurement (max-over-ranks time, summed units) and, optionally, to gather results
 to one rank for checking - never inside the demodulation itself.
-Backend: "nccl" (RCCL over xGMI) on GPUs, "gloo" on CPU (tests).
+The helpers use whichever torch.distributed backend the caller initialised (bench.py
+uses gloo over host TCP, for the timing barrier and the max/sum of the timings only; the
+tests use gloo on CPU); nothing here runs on the demodulation path, so no RCCL is needed.
 """
 from __future__ import annotations
 

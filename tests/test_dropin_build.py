@@ -35,7 +35,11 @@ def test_dropin_symbols_exported():
         pytest.skip("library not built")
     out = subprocess.run(["nm", "-DC", LIB], capture_output=True, text=True).stdout
     for sym in ("lora_phy::lora_demod_init(", "lora_phy::lora_demod_free(", "lora_phy::lora_demodulate(",
-                "lora_phy::lora_modulate(", "lora_phy::lora_encode(", "lora_phy::lora_decode(", "genChirp("):
+                "lora_phy::lora_modulate(", "lora_phy::lora_encode(", "lora_phy::lora_decode(", "genChirp(",
+                # the workspace API (phy.hpp:102-156)
+                "lora_phy::init(", "lora_phy::reset(", "lora_phy::encode(", "lora_phy::decode(",
+                "lora_phy::modulate(", "lora_phy::demodulate(", "lora_phy::estimate_offsets(",
+                "lora_phy::compensate_offsets(", "lora_phy::get_last_metrics(", "lora_phy::detail::release("):
         assert any(sym in line and " T " in line for line in out.splitlines()), sym
 
 
@@ -44,3 +48,25 @@ def test_e2e_program_links():
         pytest.skip("tests/native/e2e_dropin not built")
     r = subprocess.run(["ldd", E2E], capture_output=True, text=True)
     assert "liblora_mi355x.so" in r.stdout and "not found" not in r.stdout, r.stdout
+
+
+def test_workspace_api_compiles_for_rx_runner_style_caller(tmp_path):
+    """runners/rx_runner.cpp:93-122's use of the workspace API (C++11, the reference's
+    standard) against include/compat."""
+    if not shutil.which("g++"):
+        pytest.skip("no g++")
+    src = tmp_path / "rx.cpp"
+    src.write_text(
+        "#include <lora_phy/phy.hpp>\n#include <vector>\nusing namespace lora_phy;\n"
+        "int main(){ std::vector<uint16_t> symbols(8); std::vector<std::complex<float>> fft_in(128), fft_out(128),\n"
+        " samples(1280);\n lora_params params{}; params.sf = 7; params.bw = bandwidth::bw_125; params.cr = 1;\n"
+        " lora_workspace ws{}; ws.symbol_buf = symbols.data(); ws.fft_in = fft_in.data(); ws.fft_out = fft_out.data();\n"
+        " if (init(&ws, &params) != 0) return 1;\n"
+        " ssize_t n = demodulate(&ws, samples.data(), samples.size(), symbols.data(), symbols.size());\n"
+        " std::vector<uint8_t> decoded(4); ssize_t b = decode(&ws, symbols.data(), n, decoded.data(), decoded.size());\n"
+        " const lora_metrics* m = get_last_metrics(&ws); estimate_offsets(&ws, samples.data(), samples.size());\n"
+        " compensate_offsets(&ws, samples.data(), samples.size()); reset(&ws);\n"
+        " return (int)(b + (m->crc_ok ? 1 : 0)); }\n")
+    r = subprocess.run(["g++", "-std=c++11", "-fsyntax-only", "-I", os.path.join(REPO, "include", "compat"), str(src)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
