@@ -1354,6 +1354,284 @@ int row_complex() {
   return lds_row<SF>();
 }
 
+// ---- the speculative pipeline's estimate kernels, one lane group per symbol -----------
+// k_est_split<SF, MODE, SPEC>: stage 0 (SPEC 1, pre-pass) and stage 2 (SPEC 2, exact
+// estimate + certification) of the pipeline for LEGACY osr-1 unwindowed frames at SF 6-9
+// (2T <= 64 lanes per frame: a wave holds 64 / 2T frames).  The work and the arithmetic
+// are k_est_fast's; the layout differs: symbols 0 and 1 of a frame go to two lane groups
+// side by side (the offset estimate's two transforms and detector tails, then the two
+// sync symbols, run concurrently on different lanes instead of one after the other in
+// one group), and the certification spreads over both groups.  Twice the waves with half
+// the registers each: these kernels are latency-bound chains per frame.
+#ifndef LORA_EST_SPLIT
+#define LORA_EST_SPLIT 1
+#endif
+// One data symbol s = 2 + j of frame f exactly as the reference computes it (scaled
+// samples, glibc-faithful rotation, kissfft order; LoRaDemod.cpp:137-175) by a T-lane
+// group, written to the output (k_est_split's recomputation of uncertified symbols).
+template <int SF, int MODE>
+__device__ __attribute__((noinline)) void recompute_symbol(const KArgs& a, const cf* __restrict__ x, int64_t f, int j,
+                                                          const FrameParams& q, cf* row, int l, bool valid) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P;
+  const int s = 2 + j;
+  int64_t base;
+  int cg;
+  sym_base(s, N, a.frame_len, q.t_off, base, cg);
+  const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off);
+  cf in[P], z[P];
+  gather_points<SF>(a, x + base, l, 1, N, cg, 1, MODE == 0, q.scaled ? q.scale : 1.0f, in);
+  rotate_place<SF, true>(in, z, start, q.rate, false, a.win, l);
+  uint64_t key = fft_key<SF, false>(z, row, l, a);
+  key = group_max(key, T);
+  if (l == 0 && valid) {
+    if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)key_index(key);
+    atomicAdd(a.spec_fix, 1u);
+  }
+  wave_sync();  // row is rewritten by the next transform
+}
+
+#ifndef LORA_EST_SPLIT_W2
+#define LORA_EST_SPLIT_W2 3  // waves per SIMD of the stage-2 kernel (the certification adds fp64 state)
+#endif
+template <int SF, int MODE, int SPEC>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPEC == 1 ? 4 : LORA_EST_SPLIT_W2)))
+LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P;
+  constexpr int FPW = 64 / (2 * T);  // frames per wave (= block)
+  static_assert(SPEC == 1 || SPEC == 2, "pipeline stages 0 and 2");
+  static_assert(2 * T <= 64 && P == 16, "SF 6-9");
+  constexpr bool dech = MODE == 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ FrameParams sp[FPW];
+  __shared__ float tail[FPW][2][4];  // per frame and symbol: index, fractional index, phase, -
+  __shared__ uint32_t sws[FPW][2];
+  // SPEC 2: one bit per data symbol that failed certification (frames of up to
+  // kSpecChunks * T data symbols)
+  __shared__ unsigned long long fmask[SPEC == 2 ? FPW : 1][SPEC == 2 ? T : 1];
+  const int tid = threadIdx.x;
+  LORA_ESTAMP(5, true);
+  LORA_ESTAMP(0, false);
+  const int g2 = tid / T;     // lane group: frame slot fg, symbol sym
+  const int fg = g2 >> 1;
+  const int sym = g2 & 1;
+  const int l = tid % T;      // lane within the group
+  const int l2 = tid % (2 * T);  // lane within the frame's two groups
+  const int64_t f0 = (int64_t)blockIdx.x * FPW + fg;
+  const bool valid = f0 < frames;
+  const int64_t f = valid ? f0 : frames - 1;
+  const cf* __restrict__ x = a.iq + f * a.frame_stride;
+  cf* row = reinterpret_cast<cf*>(smem) + (size_t)g2 * rowc;
+  const int per = a.total - 2;
+  // reduce over the frame's 2T lanes (the two groups of a frame are adjacent)
+  auto frame_max = [&](float v) {
+#pragma unroll
+    for (int o = T; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+  };
+  float maxv = 0.0f;
+  if constexpr (SPEC == 2) {
+    // LoRaDemod.cpp:59-67 from the pre-pass's slot (samples outside the data windows) and
+    // every data window's maximum (the demod's (margin, max) pairs)
+    maxv = __uint_as_float(a.maxbits[f]);
+    const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
+#pragma unroll 4
+    for (int j = l2; j < per; j += 2 * T) maxv = fmaxf(maxv, mg[j].y);
+    maxv = frame_max(maxv);
+  }
+  const int scaled = maxv > 1.0f;
+  const float scale = scaled ? 1.0f / maxv : 1.0f;
+  LORA_ESTAMP(1, false);
+  if (SPEC == 2 && !scaled && l2 == 0 && valid) {
+    // no rescaling: the pre-pass estimate and its sync word are the reference's
+    const FrameParams qs = a.fp_spec[f];
+    a.fp[f] = qs;
+    if (a.cfo) a.cfo[f] = qs.cfo;
+    if (a.toff) a.toff[f] = qs.toff;
+    if (a.max_amp) a.max_amp[f] = maxv;
+    if (a.sync) a.sync[f] = (uint8_t)qs.pad0;
+  }
+  FrameParams q;
+  if (SPEC == 2 && !scaled) {
+    q = a.fp_spec[f];
+  } else {
+    // LoRaDemod.cpp:79-123 (osr 1: one phase per symbol) for symbol `sym` of the frame
+    cf in[P], z[P];
+    gather_points<SF>(a, x + (int64_t)sym * N, l, 1, N, 0, 1, dech, scale, in);
+    float mo = 0.0f;  // SPEC 1: max(|I|,|Q|) over symbols 0/1 (this group's gathers)
+    if constexpr (SPEC == 1) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) mo = amax3(mo, in[k]);
+      asm volatile("" : "+v"(mo));
+    }
+    rotate_place<SF, false>(in, z, 0.0f, 0.0f, false, a.win, l);
+    uint64_t key = fft_key<SF, true>(z, row, l, a);
+    key = group_max(key, T);
+    if (l == 0) {
+      // LoRaDetector.hpp:60-71 tail on the winning bin, and arg(bin) (LoRaDemod.cpp:124)
+      const uint32_t idx = key_index(key);
+      const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
+      const cf L = row[lds_slot<SF>((int)im1)], R = row[lds_slot<SF>((int)ip1)], B = row[lds_slot<SF>((int)idx)];
+      float pw, fi;
+      detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
+      // best over the (single) osr phase from best_p = -1e30 (LoRaDemod.cpp:86-101)
+      const bool take = pw > -1e30f;
+      tail[fg][sym][0] = take ? (float)idx : 0.0f;
+      tail[fg][sym][1] = take ? fi : 0.0f;
+      tail[fg][sym][2] = lm_atan2f(take ? B.im : 0.0f, take ? B.re : 0.0f);
+    }
+    wave_sync();
+    LORA_ESTAMP(2, false);
+    if (l2 == 0) {
+      // LoRaDemod.cpp:105-135 in the reference's order: symbol 0's terms, then symbol 1's
+      float sum_index = 0.0f, phase_diff = 0.0f;
+      sum_index += tail[fg][0][0] + tail[fg][0][1];
+      sum_index += tail[fg][1][0] + tail[fg][1][1];
+      float d = tail[fg][1][2] - tail[fg][0][2];
+      while (d > PI_F) d -= 2.0f * PI_F;
+      while (d < -PI_F) d += 2.0f * PI_F;
+      phase_diff += d;
+      const float avg_index = sum_index / 2.0f;
+      const float cfo_coarse = avg_index / (float)N;
+      const float cfo_fine = (phase_diff / 1.0f) / (2.0f * PI_F * (float)N);
+      const float cfo = cfo_coarse + cfo_fine;
+      const float frac = avg_index - floorf(avg_index + 0.5f);
+      const float avg_t = (float)0u / 2.0f;
+      const float toff = avg_t - frac * (float)N * 1.0f;
+      FrameParams qe;
+      qe.cfo = cfo;
+      qe.toff = toff;
+      qe.t_off = (int)roundf(toff);
+      qe.rate = -2.0f * PI_F * cfo / (float)N;
+      qe.scale = scale;
+      qe.scaled = scaled;
+      qe.pad0 = qe.pad1 = 0;
+      sp[fg] = qe;
+      if (valid) {
+        if constexpr (SPEC == 1) {
+          a.fp_spec[f] = qe;
+        } else {
+          a.fp[f] = qe;
+          if (a.cfo) a.cfo[f] = cfo;
+          if (a.toff) a.toff[f] = toff;
+          if (a.max_amp) a.max_amp[f] = maxv;
+        }
+      }
+    }
+    wave_sync();
+    q = sp[fg];
+    LORA_ESTAMP(3, false);
+    if constexpr (SPEC == 1) {
+      // the samples outside every data-symbol window of these offsets: [0, 2N) came with
+      // the gathers above; a positive t_off's [2N, 2N + t_off) and the frame's tail here
+      int64_t b2, bl;
+      int cg;
+      sym_base(2, N, a.frame_len, q.t_off, b2, cg);
+      sym_base(a.total - 1, N, a.frame_len, q.t_off, bl, cg);
+      const int64_t xend = bl + N;
+      float m = mo;
+      for (int64_t j = 2 * (int64_t)N + l2; j < b2; j += 2 * T) {
+        cf v = x[j];
+        if (dech) v = cmul(v, a.down[j % N]);
+        m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+      }
+      for (int64_t j = xend + l2; j < a.frame_len; j += 2 * T) {
+        cf v = x[j];
+        if (dech) v = cmul(v, a.down[j % N]);
+        m = fmaxf(m, fmaxf(fabsf(v.re), fabsf(v.im)));
+      }
+      m = frame_max(m);
+      if (l2 == 0 && valid) a.spec_max[f] = __float_as_uint(m);
+      // already above 1: rescaled, stage 2 recomputes the estimate and the sync word
+      if (m > 1.0f) {  // frame-uniform
+        LORA_ESTAMP(4, false);
+        LORA_ESTAMP(6, true);
+        return;
+      }
+    }
+    // the sync symbols with the estimated offsets (LoRaDemod.cpp:137-168, 177-192),
+    // symbol `sym` on this group
+    {
+      int64_t base;
+      int cg;
+      sym_base(sym, N, a.frame_len, q.t_off, base, cg);
+      const float start = q.rate * ((float)((uint32_t)sym * (uint32_t)N) + (float)q.t_off);
+      gather_points<SF>(a, x + base, l, 1, N, cg, 1, dech, q.scaled ? q.scale : 1.0f, in);
+      rotate_place<SF, true>(in, z, start, q.rate, false, a.win, l);
+      uint64_t k2 = fft_key<SF, false>(z, row, l, a);
+      k2 = group_max(k2, T);
+      if (l == 0) sws[fg][sym] = key_index(k2);
+      wave_sync();
+    }
+    if (l2 == 0 && valid) {
+      const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
+      const uint8_t word = (uint8_t)((((sws[fg][0] >> shift) & 0x0f) << 4) | ((sws[fg][1] >> shift) & 0x0f));
+      if constexpr (SPEC == 1)
+        a.fp_spec[f].pad0 = word;  // the pre-pass sync word, final when the frame is not rescaled
+      else if (a.sync)
+        a.sync[f] = word;
+    }
+    LORA_ESTAMP(4, false);
+    if constexpr (SPEC == 1) {
+      LORA_ESTAMP(6, true);
+      return;
+    }
+  }
+  if constexpr (SPEC == 2) {
+    // certification of the data symbols (k_est_fast<SPEC = 2> states the bound)
+    const FrameParams qs = a.fp_spec[f];
+    const bool same_t = qs.t_off == q.t_off;
+    for (int w = l2; w < T; w += 2 * T) fmask[fg][w] = 0;
+    wave_sync();
+    {
+      const double u = 1.0 / 16777216.0;
+      const double E = (8.0 * SF + 32.0) * u;
+      const double drate = fabs((double)q.rate - (double)qs.rate);
+      const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
+      const double tabs = (double)abs(q.t_off);
+      const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
+#pragma unroll 1
+      for (int j = l2; j < per; j += 2 * T) {
+        const float2 v = mg[j];
+        const double n1 = 2.0 * N * (double)v.y;
+        const double L = (double)(3 + j) * N + tabs;
+        const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
+        const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 6e-6;
+        const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
+        if (!(same_t && (double)v.x > 4.0 * B)) atomicOr(&fmask[fg][j >> 6], 1ull << (j & 63));
+      }
+    }
+    wave_sync();
+    LORA_ESTAMP(7, false);
+    // recompute the failures exactly: the frame's two groups take turns (out of line: a
+    // rare path whose registers must not weigh on the rest of the kernel)
+    int k = 0;
+    for (int w = 0; w < (per + 63) >> 6; ++w) {
+      unsigned long long m = fmask[fg][w];
+      while (m) {
+        const int j = w * 64 + __builtin_ctzll(m);
+        m &= m - 1;
+        if ((k++ & 1) != sym) continue;  // group-uniform
+        recompute_symbol<SF, MODE>(a, x, f, j, q, row, l, valid);
+      }
+    }
+    LORA_ESTAMP(6, true);
+  }
+}
+
+template <int SF, int MODE, int SPEC>
+bool launch_est_split(const KArgs& a, int64_t frames, hipStream_t st) {
+  using G = Geo<SF>;
+  constexpr int FPW = 64 / (2 * G::T);
+  const int rowc = row_complex<SF>();
+  const size_t lds = sizeof(cf) * (size_t)(2 * FPW) * rowc;
+  const int64_t grid = (frames + FPW - 1) / FPW;
+  hipLaunchKernelGGL((k_est_split<SF, MODE, SPEC>), dim3((unsigned)grid), dim3(64), lds, st, a, frames, rowc);
+  return true;
+}
+
+
 template <int SF, int MODE, int SPEC = 0>
 bool launch_est_mode(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
@@ -1419,6 +1697,12 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
     return false;
   } else {
     const int64_t work = frames * (int64_t)(a.total - 2);
+    if constexpr (SF <= 9 && LORA_EST_SPLIT) {
+      if (stage == 0)
+        return a.dechirp ? launch_est_split<SF, 0, 1>(a, frames, st) : launch_est_split<SF, 1, 1>(a, frames, st);
+      if (stage == 2)
+        return a.dechirp ? launch_est_split<SF, 0, 2>(a, frames, st) : launch_est_split<SF, 1, 2>(a, frames, st);
+    }
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
     if (stage == 1)
       return a.dechirp ? launch_spec_demod<SF, 0>(a, work, st) : launch_spec_demod<SF, 1>(a, work, st);

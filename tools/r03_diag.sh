@@ -11,6 +11,12 @@ for sf in 7 12; do
   LORA_MI355X_LIB=$V/stamps.so timeout -k 10 180 python tools/stamps.py $sf > $OUT/stamps_sf$sf.json 2> $OUT/stamps_sf$sf.err || { tail -5 $OUT/stamps_sf$sf.err; exit 1; }
   cat $OUT/stamps_sf$sf.json
 done
+echo "== ab nosplit $(date +%T)"
+LORA_MI355X_LIB=$V/nosplit.so timeout -k 10 300 python bench.py --no-cpu --no-channels --no-fast --no-variants > $OUT/ab_nosplit.json 2> $OUT/ab_nosplit.err || { tail -5 $OUT/ab_nosplit.err; exit 1; }
+echo "== kt7 $(date +%T)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt7 -o run -- python bench.py --steps 20 --warmup 3 --no-cpu --no-channels --no-fast --no-variants --no-sf12 > $OUT/kt7.log 2>&1 || { tail -20 $OUT/kt7.log; exit 1; }
+echo "== kt12 $(date +%T)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt12 -o run -- python bench.py --steps 6 --warmup 2 --sf12-only > $OUT/kt12.log 2>&1 || { tail -20 $OUT/kt12.log; exit 1; }
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
            "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM" \
