@@ -85,7 +85,8 @@ struct lora_metrics {
 namespace detail {
 /* Device side of a workspace: an API- or LEGACY-mode plan, one device allocation (IQ |
  * symbols | per-frame outputs | batch workspace), pinned host staging for the same
- * layout, and a stream. */
+ * layout, a stream, and a private AQL queue on which each frame's kernels are dispatched
+ * without a HIP runtime call (so without a host allocation). */
 struct device_state {
   unsigned sf{};
   unsigned plan_osr{};
@@ -98,6 +99,7 @@ struct device_state {
   size_t bytes{};    // capacity of dev and host
   size_t samples{};  // IQ capacity in complex samples
   void* stream{};    // hipStream_t
+  void* aql{};       // lora::AqlQueue (csrc/lora_aql.hip); null: frames go through HIP
 };
 void release(device_state& d);
 }  // namespace detail

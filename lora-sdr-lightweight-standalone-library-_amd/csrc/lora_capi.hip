@@ -41,6 +41,10 @@
 using lora::cf;
 using lora::KArgs;
 
+namespace lora {
+thread_local LaunchRecord* t_launch_record = nullptr;
+}  // namespace lora
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -988,6 +992,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   }
   int kernels = 0;
   int rc = LORA_OK;
+  if (p.mode == LORA_MODE_RAW && lora::t_launch_record) lora::t_launch_record->bad = true;
   if (p.mode == LORA_MODE_RAW) {
     // detector only: per-frame outputs are defined as 0
     hipError_t e = hipSuccess;
@@ -1035,17 +1040,17 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
       kernels |= LORA_KERNEL_FRAME_MAX | (max_wave ? LORA_KERNEL_FRAME_MAX_WAVE : 0);
       ProfScope ps(plan, 0, st);
       if (max_wave)
-        hipLaunchKernelGGL(k_frame_max_wave, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, st, a, frames,
+        lora::launch(k_frame_max_wave, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, st, a, frames,
                            maxbits);
       else
-        hipLaunchKernelGGL(k_frame_max, dim3((unsigned)(frames * bpf)), dim3(256), 0, st, a, bpf, chunk, maxbits);
+        lora::launch(k_frame_max, dim3((unsigned)(frames * bpf)), dim3(256), 0, st, a, bpf, chunk, maxbits);
     }
     if (p.mode != LORA_MODE_RAW) {
       ProfScope ps(plan, 1, st);
       kernels |= LORA_KERNEL_ESTIMATE;
       if (!lora::launch_est_fast(a, frames, st)) {
         kernels |= LORA_KERNEL_GENERIC;
-        hipLaunchKernelGGL(k_estimate, dim3((unsigned)frames), dim3(256), sizeof(cf) * plan->N, st, a);
+        lora::launch(k_estimate, dim3((unsigned)frames), dim3(256), sizeof(cf) * plan->N, st, a);
       }
     }
     const int64_t work = frames * per;

@@ -1627,7 +1627,7 @@ bool launch_est_split(const KArgs& a, int64_t frames, hipStream_t st) {
   const int rowc = row_complex<SF>();
   const size_t lds = sizeof(cf) * (size_t)(2 * FPW) * rowc;
   const int64_t grid = (frames + FPW - 1) / FPW;
-  hipLaunchKernelGGL((k_est_split<SF, MODE, SPEC>), dim3((unsigned)grid), dim3(64), lds, st, a, frames, rowc);
+  launch(k_est_split<SF, MODE, SPEC>, dim3((unsigned)grid), dim3(64), lds, st, a, frames, rowc);
   return true;
 }
 
@@ -1646,7 +1646,7 @@ bool launch_est_mode(const KArgs& a, int64_t frames, hipStream_t st) {
                             (int)lds) != hipSuccess)
       return false;
   const int64_t grid = (frames + SPB - 1) / SPB;
-  hipLaunchKernelGGL((k_est_fast<SF, MODE, SPEC>), dim3((unsigned)grid), dim3(BLOCK), lds, st, a, frames, rowc);
+  launch(k_est_fast<SF, MODE, SPEC>, dim3((unsigned)grid), dim3(BLOCK), lds, st, a, frames, rowc);
   return true;
 }
 
@@ -1669,7 +1669,7 @@ bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return false;
   const int64_t grid = (work + G::SPW - 1) / G::SPW;
-  hipLaunchKernelGGL((k_demod_fast<SF, MODE, FAST, SPEC>), dim3((unsigned)grid), dim3(256), lds, st, a, s0, work,
+  launch(k_demod_fast<SF, MODE, FAST, SPEC>, dim3((unsigned)grid), dim3(256), lds, st, a, s0, work,
                      rowc);
   return true;
 }
@@ -1686,7 +1686,7 @@ bool launch_spec_demod(const KArgs& a, int64_t work, hipStream_t st) {
                             (int)lds) != hipSuccess)
       return false;
   const int64_t grid = (work + G::SPW * R - 1) / (G::SPW * R);
-  hipLaunchKernelGGL((k_spec_demod<SF, MODE, R>), dim3((unsigned)grid), dim3(256), lds, st, a, work, rowc);
+  launch(k_spec_demod<SF, MODE, R>, dim3((unsigned)grid), dim3(256), lds, st, a, work, rowc);
   return true;
 }
 

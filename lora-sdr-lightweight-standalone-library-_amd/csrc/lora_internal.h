@@ -102,4 +102,73 @@ bool launch_spec(const KArgs& a, int64_t frames, int stage, hipStream_t st);
 // (frames with >= 2 whole symbols; false = not covered, use k_estimate).
 bool launch_est_fast(const KArgs& a, int64_t frames, hipStream_t st);
 
+// ---- launch recording: the C++ drop-in's allocation-free dispatch (lora_aql.hip) -------
+// Every kernel launch of lora_demod_batch goes through lora::launch.  Normally that is
+// hipLaunchKernelGGL; while a thread has a LaunchRecord installed (t_launch_record) the
+// launch is recorded instead - kernel host stub, 1-D grid and block, dynamic LDS, and the
+// explicit kernel arguments packed at their C++ ABI offsets (what the code object's
+// kernarg metadata lists, tests/test_aql_kernargs.py) - and lora_aql.hip later writes it
+// as an AQL dispatch packet into a queue of its own, with no HIP call and so no host
+// allocation per call (the reference's no_alloc_test.cpp:90-99 guard).
+struct RecordedLaunch {
+  static constexpr unsigned kArgBytes = 384;  // explicit arguments (the kernels use <= 264)
+  const void* fn;
+  unsigned grid, block, lds, arg_bytes;
+  alignas(16) unsigned char args[kArgBytes];
+};
+struct LaunchRecord {
+  static constexpr int kMax = 6;
+  RecordedLaunch l[kMax];
+  int n = 0;
+  bool bad = false;  // an unsupported launch (more than kMax, a 2-D/3-D shape, a memset)
+};
+extern thread_local LaunchRecord* t_launch_record;
+
+template <class... P>
+void record_launch(LaunchRecord& r, const void* fn, dim3 grid, dim3 block, size_t lds, P... v) {
+  if (r.n >= LaunchRecord::kMax || grid.y != 1 || grid.z != 1 || block.y != 1 || block.z != 1) {
+    r.bad = true;
+    return;
+  }
+  RecordedLaunch& L = r.l[r.n++];
+  L.fn = fn;
+  L.grid = grid.x;
+  L.block = block.x;
+  L.lds = (unsigned)lds;
+  size_t off = 0;
+  auto put = [&](const void* p, size_t size, size_t align) {
+    off = (off + align - 1) / align * align;
+    if (off + size > RecordedLaunch::kArgBytes) {
+      r.bad = true;
+      return;
+    }
+    __builtin_memcpy(L.args + off, p, size);
+    off += size;
+  };
+  (put(&v, sizeof(P), alignof(P)), ...);
+  L.arg_bytes = (unsigned)off;
+}
+
+template <class... P, class... A>
+inline void launch(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t st, A&&... args) {
+  static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+  if (LaunchRecord* r = t_launch_record) {
+    record_launch<P...>(*r, reinterpret_cast<const void*>(k), grid, block, lds, static_cast<P>(args)...);
+    return;
+  }
+  hipLaunchKernelGGL(k, grid, block, lds, st, static_cast<P>(args)...);
+}
+
+// A private AQL queue on the device's HSA agent (lora_aql.hip).  aql_run writes the
+// record's launches as dispatch packets (barrier bit: in order; system-scope acquire on
+// the first and release on the last, so host-resident inputs and outputs are coherent),
+// rings the doorbell once and waits for the last packet's completion signal.  Kernel
+// objects are found once per kernel in the code object the HIP runtime loaded
+// (hipKernelNameRefByPtr + the HSA loader extension) and cached.  Returns 0 or a negative
+// error code.
+struct AqlQueue;
+int aql_create(int device, AqlQueue** out);
+int aql_run(AqlQueue* q, const LaunchRecord& r);
+void aql_destroy(AqlQueue* q);
+
 }  // namespace lora

@@ -158,15 +158,55 @@ struct FrameOut {
   const uint16_t* syms;  // in the pinned staging
 };
 
-// One frame through lora_demod_batch: host samples -> pinned staging -> device, the
-// kernels, outputs -> pinned staging, synchronise.  No host allocation.
-bool run_frame(lora_phy::detail::device_state& g, const std::complex<float>* samples, size_t count, FrameOut& out) {
+// One frame through lora_demod_batch, synchronously.
+// With the workspace's AQL queue (lora_demod_init): the samples are copied into the pinned
+// staging, which the kernels read in place, and the outputs land there too; the batch's
+// launches are recorded and dispatched on the private queue (lora_aql.hip) - no HIP
+// runtime call, so no host allocation.  Without it: staging -> device copy, the kernels
+// on the stream, two copies back, a stream synchronisation.
+// 1 done, 0 failed, -1 a launch the queue does not take (the caller uses HIP)
+int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* samples, size_t count,
+                  FrameOut& out, int64_t nsym, const DevLayout& d) {
+  unsigned char* dev = static_cast<unsigned char*>(g.dev);
+  unsigned char* host = static_cast<unsigned char*>(g.host);
+  if (count > 0 && samples != reinterpret_cast<const std::complex<float>*>(host + d.iq))
+    std::memcpy(host + d.iq, samples, count * sizeof(std::complex<float>));
+  lora_demod_outputs o{};
+  o.symbols = reinterpret_cast<uint16_t*>(host + d.syms);
+  o.sym_stride = std::max<int64_t>(nsym, 1);
+  o.sync = host + d.sync;
+  o.cfo = reinterpret_cast<float*>(host + d.cfo);
+  o.time_offset = reinterpret_cast<float*>(host + d.toff);
+  o.max_amp = reinterpret_cast<float*>(host + d.maxa);
+  lora::LaunchRecord rec;
+  lora::t_launch_record = &rec;
+  const int64_t rc = lora_demod_batch(g.plan, reinterpret_cast<const float*>(host + d.iq), 1, (int64_t)count,
+                                      (int64_t)count, &o, dev + d.ws, d.total - d.ws, g.stream);
+  lora::t_launch_record = nullptr;
+  if (rc < 0) return 0;
+  if (rec.bad) return -1;
+  if (rec.n > 0 && lora::aql_run(static_cast<lora::AqlQueue*>(g.aql), rec) != 0) return 0;
+  out.nsym = nsym;
+  out.sync = host[d.sync];
+  std::memcpy(&out.cfo, host + d.cfo, 4);
+  std::memcpy(&out.toff, host + d.toff, 4);
+  std::memcpy(&out.max_amp, host + d.maxa, 4);
+  out.syms = reinterpret_cast<const uint16_t*>(host + d.syms);
+  return 1;
+}
+
+bool run_frame(lora_phy::detail::device_state& g, const std::complex<float>* samples, size_t count, FrameOut& out,
+               bool use_aql = true) {
   hipStream_t st = static_cast<hipStream_t>(g.stream);
   const DevLayout d = layout(g.plan, g.samples, size_t(1) << g.sf);
   unsigned char* dev = static_cast<unsigned char*>(g.dev);
   unsigned char* host = static_cast<unsigned char*>(g.host);
   const int64_t nsym = lora_demod_symbols_per_frame(g.plan, (int64_t)count);
   if (nsym < 0) return false;
+  if (g.aql && use_aql) {
+    const int r = run_frame_aql(g, samples, count, out, nsym, d);
+    if (r >= 0) return r == 1;
+  }
   if (count > 0) {
     if (samples != reinterpret_cast<const std::complex<float>*>(host + d.iq))
       std::memcpy(host + d.iq, samples, count * sizeof(std::complex<float>));
@@ -209,6 +249,7 @@ namespace lora_phy {
 
 void detail::release(device_state& g) {
   if (g.stream) hipStreamSynchronize(static_cast<hipStream_t>(g.stream));
+  if (g.aql) lora::aql_destroy(static_cast<lora::AqlQueue*>(g.aql));
   if (g.dev) hipFree(g.dev);
   if (g.host) hipHostFree(g.host);
   if (g.plan) lora_demod_plan_destroy(g.plan);
@@ -247,6 +288,16 @@ void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win, std
   FrameOut o;
   run_frame(ws->gpu, zeros, n, o);      // speculative pipeline (3+ symbols)
   run_frame(ws->gpu, zeros, ws->N, o);  // one symbol: three-launch path
+  // then the private AQL queue for lora_demodulate, and the same two frames through it
+  // (each kernel's object is looked up once, here); without it frames go through HIP
+  lora::AqlQueue* q = nullptr;
+  if (lora::aql_create(dev, &q) == 0) {
+    ws->gpu.aql = q;
+    if (!run_frame(ws->gpu, zeros, n, o) || !run_frame(ws->gpu, zeros, ws->N, o)) {
+      lora::aql_destroy(q);
+      ws->gpu.aql = nullptr;
+    }
+  }
 }
 
 void lora_demod_free(lora_demod_workspace* ws) {

@@ -62,6 +62,7 @@ int main() {
     lora_phy::lora_demod_init(&ws, sf, lora_phy::window_type::window_none, scratch.data(), scratch.size());
     init = c.get();
   }
+  const bool aql = ws.gpu.aql != nullptr;  // frames dispatched on the private AQL queue
   bool ok = true;
   for (int k = 0; k < 3; ++k) {
     Count c;
@@ -106,10 +107,10 @@ int main() {
     (void)hipStreamDestroy(st);
   }
   lora_phy::lora_demod_free(&ws);
-  std::printf("{\"roundtrip_ok\": %s, \"lora_modulate_first\": %zu, \"lora_modulate_second\": %zu, "
+  std::printf("{\"roundtrip_ok\": %s, \"aql_queue\": %s, \"lora_modulate_first\": %zu, \"lora_modulate_second\": %zu, "
               "\"lora_demod_init\": %zu, \"lora_demodulate\": [%zu, %zu, %zu], \"hip_steps_second_call\": "
               "{\"memcpy_h2d_pinned\": %zu, \"lora_demod_batch\": %zu, \"memcpy_d2h_pinned\": %zu, "
               "\"stream_sync\": %zu}}\n",
-              ok ? "true" : "false", mod1, mod2, init, dem[0], dem[1], dem[2], steps[0], steps[1], steps[2], steps[3]);
+              ok ? "true" : "false", aql ? "true" : "false", mod1, mod2, init, dem[0], dem[1], dem[2], steps[0], steps[1], steps[2], steps[3]);
   return ok ? 0 : 1;
 }
