@@ -11,7 +11,7 @@ drive the three outcomes against the CPU oracle, bit for bit:
   * recomputed symbols (exact ties between two bins, a tie in the sync pair that moves
     the time offset, low SNR), which lora_demod_spec_recomputed() counts,
 
-over SF 6-12, plus the eligibility boundary (3 symbols, kMaxBpf) and the three-launch
+over SF 6-12, plus the eligibility boundary (3 .. 2 + kSpecChunks * N/16 symbols) and the three-launch
 path the pipeline replaces.
 """
 import numpy as np
@@ -166,11 +166,11 @@ def test_amplitude_extremes(O, amd, amp):
     assert plan.last_kernels() == SPEC
 
 
-@pytest.mark.parametrize("sf,nsym,spec", [(7, 2, False), (7, 3, True), (9, 81, True), (9, 82, False),
-                                          (12, 3, True), (6, 40, True)])
+@pytest.mark.parametrize("sf,nsym,spec", [(7, 2, False), (7, 3, True), (9, 82, True), (6, 258, True),
+                                          (6, 259, False), (12, 3, True), (6, 40, True)])
 def test_eligibility_boundary(O, amd, sf, nsym, spec):
-    """The pipeline covers frames of 3 .. kMaxBpf + 1 symbols; others take the three-launch
-    path; both are exact."""
+    """The pipeline covers frames of 3 .. 2 + kSpecChunks * N/16 symbols (SF6: 258); others
+    take the three-launch path; both are exact."""
     rng = np.random.default_rng(sf * 100 + nsym)
     iq = modulated(O, rng, sf, nsym, 2, amp=1.8, noise=0.3)
     plan, _ = check(O, amd, iq, sf)
@@ -302,8 +302,8 @@ def test_max_amp_is_the_reference_frame_maximum(O, amd, sf, dechirp, path):
 def test_fused_dechirp_large_cfo_and_delay(O, amd, sf, S, F, snr_db):
     """The benchmark's path (LEGACY, fused caller dechirp): frames with a carrier offset of
     up to +-0.45 bin, a random sample delay (so t_off != 0 and every window starts at a
-    table phase cg != 0 of the paired dechirp table) and the longest eligible frames (81
-    symbols: the largest rotation phases the certification bound must cover, which for the
+    table phase cg != 0 of the paired dechirp table) and long frames (81 symbols here;
+    tests/test_gpu_scale.py goes to 514: the largest rotation phases the certification bound must cover, which for the
     recurrence-built rotation factors grows with rate * L), against the oracle on the
     caller-dechirped frames, bit for bit."""
     N = 1 << sf
