@@ -100,6 +100,7 @@ struct device_state {
   size_t samples{};  // IQ capacity in complex samples
   void* stream{};    // hipStream_t
   void* aql{};       // lora::AqlQueue (csrc/lora_aql.hip); null: frames go through HIP
+  int aql_status{};  // why there is no queue: 0, or the failing step's code (lora_internal.h)
 };
 void release(device_state& d);
 }  // namespace detail

@@ -178,46 +178,65 @@ int aql_create(int device, AqlQueue** out) {
   if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
       hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
       hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess)
-    return -19;
+    return -101;
   AqlQueue* Q = new AqlQueue();
   if (hsa_init() != HSA_STATUS_SUCCESS) {
     delete Q;
-    return -19;
+    return -102;
   }
   Q->hsa_up = true;
-  int rc = -19;
+  int rc = 0;
   do {
     bool ext = false;
-    if (hsa_system_extension_supported(HSA_EXTENSION_AMD_LOADER, 1, 3, &ext) != HSA_STATUS_SUCCESS || !ext) break;
-    if (hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(Q->loader), &Q->loader) !=
-        HSA_STATUS_SUCCESS)
+    if (hsa_system_extension_supported(HSA_EXTENSION_AMD_LOADER, 1, 3, &ext) != HSA_STATUS_SUCCESS || !ext) {
+      rc = -103;
       break;
+    }
+    if (hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(Q->loader), &Q->loader) !=
+            HSA_STATUS_SUCCESS ||
+        !Q->loader.hsa_ven_amd_loader_iterate_executables) {
+      rc = -104;
+      break;
+    }
     // HSA_AMD_AGENT_INFO_BDFID: bus << 8 | device << 3 | function
     AgentFind af{(uint32_t)(((bus & 0xff) << 8) | ((dev & 0x1f) << 3)), (uint32_t)dom};
     hsa_iterate_agents(find_gpu, &af);
-    if (!af.found) break;
+    if (!af.found) {
+      rc = -105;
+      break;
+    }
     Q->agent = af.gpu;
     PoolFind pf;
     hsa_iterate_agents(find_cpu_pool, &pf);
-    if (!pf.found) break;
-    void* ka = nullptr;
-    if (hsa_amd_memory_pool_allocate(pf.pool, (size_t)LaunchRecord::kMax * kSlotBytes, 0, &ka) != HSA_STATUS_SUCCESS)
+    if (!pf.found) {
+      rc = -106;
       break;
+    }
+    void* ka = nullptr;
+    if (hsa_amd_memory_pool_allocate(pf.pool, (size_t)LaunchRecord::kMax * kSlotBytes, 0, &ka) !=
+        HSA_STATUS_SUCCESS) {
+      rc = -107;
+      break;
+    }
     Q->kernarg = static_cast<unsigned char*>(ka);
-    if (hsa_amd_agents_allow_access(1, &Q->agent, nullptr, ka) != HSA_STATUS_SUCCESS) break;
+    if (hsa_amd_agents_allow_access(1, &Q->agent, nullptr, ka) != HSA_STATUS_SUCCESS) {
+      rc = -108;
+      break;
+    }
     uint32_t qmin = 0;
     hsa_agent_get_info(Q->agent, HSA_AGENT_INFO_QUEUE_MIN_SIZE, &qmin);
     const uint32_t qsize = qmin > 64 ? qmin : 64;
     if (hsa_queue_create(Q->agent, qsize, HSA_QUEUE_TYPE_SINGLE, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &Q->q) !=
         HSA_STATUS_SUCCESS) {
       Q->q = nullptr;
+      rc = -109;
       break;
     }
     if (hsa_signal_create(0, 0, nullptr, &Q->done) != HSA_STATUS_SUCCESS) {
       Q->done.handle = 0;
+      rc = -110;
       break;
     }
-    rc = 0;
   } while (false);
   if (rc != 0) {
     aql_destroy(Q);
@@ -241,14 +260,14 @@ int aql_run(AqlQueue* Q, const LaunchRecord& r) {
   const AqlKernel* ks[LaunchRecord::kMax];
   for (int i = 0; i < r.n; ++i) {
     ks[i] = kernel_of(Q, r.l[i].fn);
-    if (!ks[i]) return -38;
+    if (!ks[i]) return -120;
     // Kernel arguments: the explicit ones at the offsets the record packed them at, then
     // - only for kernels that use any - code object v5's implicit block at the next
     // 8-byte boundary (block counts, group sizes, remainders, global offsets, grid dims,
     // dynamic LDS size:
     // the only hidden arguments these kernels' metadata lists, tests/test_aql_kernargs.py).
     const uint32_t ex = r.l[i].arg_bytes, h = (ex + 7u) & ~7u;
-    if (ks[i]->kernarg != ex && ks[i]->kernarg != h + 256u) return -38;
+    if (ks[i]->kernarg != ex && ks[i]->kernarg != h + 256u) return -121;
     if (ks[i]->kernarg > kSlotBytes || (uint64_t)r.l[i].grid * r.l[i].block > 0xffffffffull) return -22;
   }
   hsa_queue_t* q = Q->q;

@@ -230,7 +230,10 @@ __device__ __forceinline__ void pass_regs_T2(cf* x, int k, const cf* __restrict_
 
 // The other lanes' share of one pass: read R points from LDS, run the stages,
 // either write them back or fold them into the argmax key.
-template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false, bool PAIR = false>
+// TSET: twT is known to be non-null (the speculative demod's plans always carry the
+// slot-major copies), so no fallback path is compiled.
+template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false, bool PAIR = false,
+          bool TSET = false>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
                                          uint64_t& key, const cf* __restrict__ twT = nullptr,
                                          float* second = nullptr) {
@@ -244,7 +247,7 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
 #pragma unroll
     for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
     if constexpr (R == 4 || R == 16) {
-      if (twT) {
+      if (TSET || twT) {
         if constexpr (PAIR)
           pass_regs_T2<R, MA, FMA>(xs, k, twT);
         else
@@ -513,14 +516,14 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
     // TWL: pass A's slot-major twiddles from the workgroup's LDS copy (k_demod_fast)
     const cf* twA = TWL ? twl : a.twTA;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA>(row, z, l, a.tw, key, twA, second);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA, false, TWL>(row, z, l, a.tw, key, twA, second);
     } else {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA>(row, z, l, a.tw, key, twA);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA, false, TWL>(row, z, l, a.tw, key, twA);
       block_sync<WL>();
       write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
       block_sync<WL>();
       // TWL (speculative demod): pass B's twiddles two per 16-byte load (KArgs::twTB2)
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR>(
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR, TWL>(
           row, z, l, a.tw, key, ((TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
     }
     if constexpr (KEEP) {
@@ -800,19 +803,17 @@ __device__ __forceinline__ void stamp(int k, bool real) {
 // offsets (fp_spec) on UNSCALED samples, the hardware rotation and fused multiply-adds,
 // the symbol's index, its top-bin / runner-up margin and its window's max(|I|,|Q|) (one
 // 8-byte spec_marg store), certified or recomputed exactly by k_est_fast<SPEC = 2>.  The
-// arithmetic is k_demod_fast<SF, MODE, true, true>'s.  A workgroup runs ROUNDS groups of
-// SPW symbols; the samples and table values of round r + 1 are requested as soon as
-// round r's have been dechirped (their registers are free again), so they are in flight
-// during round r's transform and reductions.
-#ifndef LORA_SPEC_ROUNDS
-#define LORA_SPEC_ROUNDS 1
+// arithmetic is k_demod_fast<SF, MODE, true, true>'s.
+// Persistent: a workgroup demodulates groups of SPW symbols blockIdx.x, blockIdx.x +
+// gstride, ... (gstride = the grid: a few workgroups per CU, launch_spec_demod).  Short
+// waves (about 4 us at SF7) left the CUs half occupied between one workgroup's end and the
+// next one's start; looping keeps every slot busy and stages the pass-A twiddles once.
+#ifndef LORA_SPEC_PERSIST
+#define LORA_SPEC_PERSIST 1
 #endif
-#ifndef LORA_SPEC_PF_TAB
-#define LORA_SPEC_PF_TAB 1  // ROUNDS > 1: prefetch the next round's table pairs too (else at its start)
-#endif
-template <int SF, int MODE, int ROUNDS>
+template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
-LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t work, int rowc) {
+LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t work, int rowc, int64_t gstride) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
   constexpr bool WL = G::WAVE_LOCAL;
@@ -823,90 +824,72 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t work, int rowc) {
   __shared__ uint64_t red[4];
   cf* rows = reinterpret_cast<cf*>(smem);
   cf* twl = rows + (size_t)SPW * rowc;
-  const int tid = threadIdx.x;
   const int per = a.total - 2;
-  const int g = tid / T;  // slot
-  const int l = tid % T;  // lane within the symbol
-  cf tv{0.0f, 0.0f};
-  if constexpr (NTW > 0) {  // issued first: it returns ahead of the symbol's gathers
-    if (tid < NTW) tv = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
+  if constexpr (NTW > 0) {
+    const int tid = threadIdx.x;
+    if (tid < NTW) twl[tid] = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
+    __syncthreads();
   }
-  // work item -> (frame, data symbol j): one 64-bit division per workgroup (scalar unit),
-  // then small per-lane quotients
-  const int64_t wb = (int64_t)blockIdx.x * (SPW * ROUNDS);
-  const int64_t fb = wb / per;
-  const int rb = (int)(wb - fb * per);
-  int64_t fr[ROUNDS];
-  int jr[ROUNDS];
-  bool vr[ROUNDS];
-  float rate[ROUNDS];
-  int toff[ROUNDS];
-#pragma unroll
-  for (int r = 0; r < ROUNDS; ++r) {
-    const int64_t w = wb + r * SPW + g;
-    vr[r] = w < work;
-    const int loc = rb + (int)((vr[r] ? w : work - 1) - wb);  // invalid lanes mirror a valid symbol
-    const int q = per >= SPW * ROUNDS ? (loc >= per ? 1 : 0) : (int)((unsigned)loc / (unsigned)per);
-    fr[r] = fb + q;
-    jr[r] = loc - q * per;
-    const FrameParams& fp = a.fp_spec[fr[r]];  // rate and t_off of every round, requested up front
-    rate[r] = fp.rate;
-    toff[r] = fp.t_off;
-  }
+  const int64_t groups = (work + SPW - 1) / SPW;
   typedef float v2f __attribute__((ext_vector_type(2)));
-  cf in[P];
-  float4 dt[P / 2];
-  auto request = [&](int r, bool iq, bool tab) {  // round r's samples (read once: nontemporal), table pairs
-    const int s = 2 + jr[r];
+  int r = 0;
+  for (int64_t grp = blockIdx.x; grp < groups; grp += gstride, ++r) {
+    // the lane index, opaque per group: left visible, the compiler hoists every lane
+    // address out of the loop and keeps them live across it (more VGPRs, spills at SF12)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int g = tid / T;  // slot
+    const int l = tid % T;  // lane within the symbol
+    LORA_STAMP(5, true);
+    LORA_STAMP(0, false);
+    // work item -> (frame, data symbol j): one 64-bit division per group (scalar unit),
+    // then a small per-lane quotient
+    const int64_t wb = grp * SPW;
+    const int64_t fb = wb / per;
+    const int rb = (int)(wb - fb * per);
+    const int64_t w = wb + g;
+    const bool valid = w < work;
+    const int loc = rb + (int)((valid ? w : work - 1) - wb);  // invalid lanes mirror a valid symbol
+    const int qf = per >= SPW ? (loc >= per ? 1 : 0) : (int)((unsigned)loc / (unsigned)per);
+    const int64_t f = fb + qf;
+    const int j = loc - qf * per;
+    const FrameParams& fp = a.fp_spec[f];
+    const float rate = fp.rate;
+    const int toff = fp.t_off;
+    const int s = 2 + j;
     int64_t base;
     int cg;
-    sym_base(s, N, a.frame_len, toff[r], base, cg);
-    if (iq) {
-      const v2f* __restrict__ xl = reinterpret_cast<const v2f*>(a.iq + fr[r] * a.frame_stride + base + l);
+    sym_base(s, N, a.frame_len, toff, base, cg);
+    // the window's samples (read once: nontemporal) and the dechirp table pairs
+    cf in[P];
+    {
+      const v2f* __restrict__ xl = reinterpret_cast<const v2f*>(a.iq + f * a.frame_stride + base + l);
 #pragma unroll
       for (int q = 0; q < P; ++q) {
         const v2f v = __builtin_nontemporal_load(xl + T * q);
         in[q] = cf{v.x, v.y};
       }
     }
-    if constexpr (MODE == 0) {
-      if (tab) {
-        const float4* __restrict__ dp = reinterpret_cast<const float4*>(a.downP) + cg + l;
-#pragma unroll
-        for (int pp = 0; pp < P / 2; ++pp) dt[pp] = dp[pp * (N + T)];
-      }
-    }
-  };
-  request(0, true, true);
-  if constexpr (NTW > 0) {
-    if (tid < NTW) twl[tid] = tv;
-    __syncthreads();
-  }
-#pragma unroll
-  for (int r = 0; r < ROUNDS; ++r) {
-    LORA_STAMP(5, true);
-    LORA_STAMP(0, false);
-    if (r > 0 && !LORA_SPEC_PF_TAB) request(r, false, true);
     // caller-side dechirp (e2e_chain_test.cpp:88-93) with the reference's products, the
     // window's max(|I|,|Q|) of exactly these samples, then the rotation
     if constexpr (MODE == 0) {
+      const float4* __restrict__ dp = reinterpret_cast<const float4*>(a.downP) + cg + l;
 #pragma unroll
       for (int pp = 0; pp < P / 2; ++pp) {
-        in[2 * pp] = cmul(in[2 * pp], cf{dt[pp].x, dt[pp].y});
-        in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
+        const float4 d = dp[pp * (N + T)];
+        in[2 * pp] = cmul(in[2 * pp], cf{d.x, d.y});
+        in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{d.z, d.w});
       }
     }
     float pm = 0.0f;
 #pragma unroll
     for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
     LORA_STAMP(1, false);
-    const int s = 2 + jr[r];
-    const float start = rate[r] * ((float)((uint32_t)s * (uint32_t)N) + (float)toff[r]);
+    const float start = rate * ((float)((uint32_t)s * (uint32_t)N) + (float)toff);
     cf z[P];
-    rotate_place<SF, true, true, true>(in, z, start, rate[r], false, a.win, l);
+    rotate_place<SF, true, true, true>(in, z, start, rate, false, a.win, l);
     asm volatile("" : "+v"(pm));
     LORA_STAMP(2, false);
-    if (r + 1 < ROUNDS) request(r + 1, true, LORA_SPEC_PF_TAB);  // into the registers the dechirp just freed
     float sec = 0.0f;
     const uint64_t lkey = fft_key<SF, false, true, (NTW > 0)>(z, rows + (size_t)g * rowc, l, a, &sec, twl);
     LORA_STAMP(3, false);
@@ -914,13 +897,13 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t work, int rowc) {
     // runner-up over the symbol: the top lane offers its own runner-up, the others their best
     float r2 = lkey == key ? sec : key_value(lkey);
     group_reduce2<SF>(r2, pm, tid, reinterpret_cast<float*>(smem + 64));
-    if (l == 0 && vr[r]) {
-      if (a.syms) a.syms[fr[r] * a.sym_stride + jr[r]] = (uint16_t)key_index(key);
-      reinterpret_cast<float2*>(a.spec_marg)[fr[r] * per + jr[r]] = make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm);
+    if (l == 0 && valid) {
+      if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)key_index(key);
+      reinterpret_cast<float2*>(a.spec_marg)[f * per + j] = make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm);
     }
     LORA_STAMP(4, false);
     LORA_STAMP(6, true);
-    if (r + 1 < ROUNDS) block_sync<WL>();  // the rows (and group_reduce2's scratch) are rewritten next round
+    block_sync<WL>();  // the rows (and group_reduce2's scratch) are rewritten by the next group
   }
 }
 
@@ -1674,19 +1657,37 @@ bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   return true;
 }
 
+// Persistent grid of the speculative demod: kSpecWgPerCu workgroups per CU (the LDS rows
+// allow four at every SF), or one per group when there are fewer groups.
+#ifndef LORA_SPEC_WG_PER_CU
+#define LORA_SPEC_WG_PER_CU 4
+#endif
+int device_cus() {
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 template <int SF, int MODE>
 bool launch_spec_demod(const KArgs& a, int64_t work, hipStream_t st) {
   using G = Geo<SF>;
-  constexpr int R = LORA_SPEC_ROUNDS;
   const int rowc = row_complex<SF>();
   const size_t lds = sizeof(cf) * ((size_t)G::SPW * rowc + demod_twl_entries<SF, true>());
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
       return false;
-  const int64_t grid = (work + G::SPW * R - 1) / (G::SPW * R);
-  launch(k_spec_demod<SF, MODE, R>, dim3((unsigned)grid), dim3(256), lds, st, a, work, rowc);
+  const int64_t groups = (work + G::SPW - 1) / G::SPW;
+  const int64_t cap = LORA_SPEC_PERSIST ? (int64_t)device_cus() * LORA_SPEC_WG_PER_CU : groups;
+  const int64_t grid = groups < cap ? groups : cap;
+  launch(k_spec_demod<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, work, rowc, grid);
   return true;
 }
 
@@ -1700,8 +1701,6 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
     if constexpr (SF <= 9 && LORA_EST_SPLIT) {
       if (stage == 0)
         return a.dechirp ? launch_est_split<SF, 0, 1>(a, frames, st) : launch_est_split<SF, 1, 1>(a, frames, st);
-      if (stage == 2)
-        return a.dechirp ? launch_est_split<SF, 0, 2>(a, frames, st) : launch_est_split<SF, 1, 2>(a, frames, st);
     }
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
     if (stage == 1)

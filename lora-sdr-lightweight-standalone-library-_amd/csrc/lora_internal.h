@@ -164,8 +164,9 @@ inline void launch(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStream
 // the first and release on the last, so host-resident inputs and outputs are coherent),
 // rings the doorbell once and waits for the last packet's completion signal.  Kernel
 // objects are found once per kernel in the code object the HIP runtime loaded
-// (hipKernelNameRefByPtr + the HSA loader extension) and cached.  Returns 0 or a negative
-// error code.
+// (hipKernelNameRefByPtr + the HSA loader extension) and cached.  Return 0 or a negative
+// code naming the step that failed (aql_create: -101 .. -110; aql_run: -22 an unusable
+// record, -120 a kernel object not found, -121 an unexpected kernarg layout, -62 timeout).
 struct AqlQueue;
 int aql_create(int device, AqlQueue** out);
 int aql_run(AqlQueue* q, const LaunchRecord& r);

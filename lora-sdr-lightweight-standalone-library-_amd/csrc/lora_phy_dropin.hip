@@ -164,7 +164,8 @@ struct FrameOut {
 // launches are recorded and dispatched on the private queue (lora_aql.hip) - no HIP
 // runtime call, so no host allocation.  Without it: staging -> device copy, the kernels
 // on the stream, two copies back, a stream synchronisation.
-// 1 done, 0 failed, -1 a launch the queue does not take (the caller uses HIP)
+// 1 done, 0 failed, -1 a launch the queue does not take (the caller uses HIP), < -1 the
+// queue's error code (lora::aql_run)
 int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* samples, size_t count,
                   FrameOut& out, int64_t nsym, const DevLayout& d) {
   unsigned char* dev = static_cast<unsigned char*>(g.dev);
@@ -185,7 +186,10 @@ int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* 
   lora::t_launch_record = nullptr;
   if (rc < 0) return 0;
   if (rec.bad) return -1;
-  if (rec.n > 0 && lora::aql_run(static_cast<lora::AqlQueue*>(g.aql), rec) != 0) return 0;
+  if (rec.n > 0) {
+    const int e = lora::aql_run(static_cast<lora::AqlQueue*>(g.aql), rec);
+    if (e != 0) return e;
+  }
   out.nsym = nsym;
   out.sync = host[d.sync];
   std::memcpy(&out.cfo, host + d.cfo, 4);
@@ -205,7 +209,7 @@ bool run_frame(lora_phy::detail::device_state& g, const std::complex<float>* sam
   if (nsym < 0) return false;
   if (g.aql && use_aql) {
     const int r = run_frame_aql(g, samples, count, out, nsym, d);
-    if (r >= 0) return r == 1;
+    if (r != -1) return r == 1;
   }
   if (count > 0) {
     if (samples != reinterpret_cast<const std::complex<float>*>(host + d.iq))
@@ -291,9 +295,15 @@ void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win, std
   // then the private AQL queue for lora_demodulate, and the same two frames through it
   // (each kernel's object is looked up once, here); without it frames go through HIP
   lora::AqlQueue* q = nullptr;
-  if (lora::aql_create(dev, &q) == 0) {
+  ws->gpu.aql_status = lora::aql_create(dev, &q);
+  if (ws->gpu.aql_status == 0) {
     ws->gpu.aql = q;
-    if (!run_frame(ws->gpu, zeros, n, o) || !run_frame(ws->gpu, zeros, ws->N, o)) {
+    const DevLayout d2 = layout(ws->gpu.plan, ws->gpu.samples, ws->N);
+    int rc = run_frame_aql(ws->gpu, zeros, n, o, lora_demod_symbols_per_frame(ws->gpu.plan, (int64_t)n), d2);
+    if (rc == 1)
+      rc = run_frame_aql(ws->gpu, zeros, ws->N, o, lora_demod_symbols_per_frame(ws->gpu.plan, (int64_t)ws->N), d2);
+    if (rc != 1) {
+      ws->gpu.aql_status = rc == -1 ? -130 : (rc == 0 ? -131 : rc);
       lora::aql_destroy(q);
       ws->gpu.aql = nullptr;
     }

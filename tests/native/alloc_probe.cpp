@@ -63,6 +63,7 @@ int main() {
     init = c.get();
   }
   const bool aql = ws.gpu.aql != nullptr;  // frames dispatched on the private AQL queue
+  const int aql_status = ws.gpu.aql_status;
   bool ok = true;
   for (int k = 0; k < 3; ++k) {
     Count c;
@@ -107,10 +108,10 @@ int main() {
     (void)hipStreamDestroy(st);
   }
   lora_phy::lora_demod_free(&ws);
-  std::printf("{\"roundtrip_ok\": %s, \"aql_queue\": %s, \"lora_modulate_first\": %zu, \"lora_modulate_second\": %zu, "
+  std::printf("{\"roundtrip_ok\": %s, \"aql_queue\": %s, \"aql_status\": %d, \"lora_modulate_first\": %zu, \"lora_modulate_second\": %zu, "
               "\"lora_demod_init\": %zu, \"lora_demodulate\": [%zu, %zu, %zu], \"hip_steps_second_call\": "
               "{\"memcpy_h2d_pinned\": %zu, \"lora_demod_batch\": %zu, \"memcpy_d2h_pinned\": %zu, "
               "\"stream_sync\": %zu}}\n",
-              ok ? "true" : "false", aql ? "true" : "false", mod1, mod2, init, dem[0], dem[1], dem[2], steps[0], steps[1], steps[2], steps[3]);
+              ok ? "true" : "false", aql ? "true" : "false", aql_status, mod1, mod2, init, dem[0], dem[1], dem[2], steps[0], steps[1], steps[2], steps[3]);
   return ok ? 0 : 1;
 }
