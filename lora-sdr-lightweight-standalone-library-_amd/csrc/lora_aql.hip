@@ -188,7 +188,9 @@ int aql_create(int device, AqlQueue** out) {
   int rc = 0;
   do {
     bool ext = false;
-    if (hsa_system_extension_supported(HSA_EXTENSION_AMD_LOADER, 1, 3, &ext) != HSA_STATUS_SUCCESS || !ext) {
+    uint16_t minor = 0;
+    if (hsa_system_major_extension_supported(HSA_EXTENSION_AMD_LOADER, 1, &minor, &ext) != HSA_STATUS_SUCCESS ||
+        !ext || minor < 3) {  // iterate_executables arrived with 1.03
       rc = -103;
       break;
     }

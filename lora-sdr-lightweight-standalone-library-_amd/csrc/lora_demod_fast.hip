@@ -146,6 +146,20 @@ __device__ __forceinline__ void block_sync() {
     __syncthreads();
 }
 
+// Speculative demod argmax keys: |X|^2's bits with the low 4 mantissa bits replaced by the
+// bin's ordinal within the lane.  Non-negative floats order like their bits, so the key
+// order is |X|^2's up to a truncation of < 16 ulp (relative 2^-19, carried by the
+// certification bound); two bins within it are never certified (their keys' values tie).
+__device__ __forceinline__ uint32_t spec_key(float m2, int ordinal) {
+  return (__float_as_uint(m2) & 0xFFFFFFF0u) | (uint32_t)ordinal;
+}
+__device__ __forceinline__ float spec_key_value(uint32_t k) { return __uint_as_float(k & 0xFFFFFFF0u); }
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // In-register DIT stages over x[0..R): positions base + MA*u, group offset k < MA.
 // Radix-2 (optional, only with MA == 1) then radix-4 stages, as kf_work unwinds.
 #ifndef LORA_UNIT_TW
@@ -232,8 +246,12 @@ __device__ __forceinline__ void pass_regs_T2(cf* x, int k, const cf* __restrict_
 // either write them back or fold them into the argmax key.
 // TSET: twT is known to be non-null (the speculative demod's plans always carry the
 // slot-major copies), so no fallback path is compiled.
+// PACK (speculative demod, LAST): instead of the 64-bit argmax key and a float runner-up,
+// the lane's best and runner-up as 32-bit keys whose high 28 bits are those of |X|^2 and
+// whose low 4 bits hold the bin's ordinal within the lane (spec_key); `key` returns
+// best | (uint64_t)second << 32.
 template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = false, bool PAIR = false,
-          bool TSET = false>
+          bool TSET = false, bool PACK = false>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
                                          uint64_t& key, const cf* __restrict__ twT = nullptr,
                                          float* second = nullptr) {
@@ -257,7 +275,21 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     }
     pass_regs<R, false, N, MA, false, FMA>(xs, k, tw);
   }
-  if constexpr (LAST) {
+  if constexpr (LAST && PACK) {
+    static_assert(NG * R == 16, "16 bins per lane: a 4-bit ordinal");
+    uint32_t best = 0, sec = 0;
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+#pragma unroll
+      for (int gg = 0; gg < NG; ++gg) {
+        const cf v = x[gg * R + u];
+        const float m2 = __builtin_fmaf(v.re, v.re, v.im * v.im);
+        const uint32_t k = spec_key(m2, u * NG + gg);
+        sec = umed3(sec, k, best);  // sec <= best: max(sec, min(k, best))
+        best = best > k ? best : k;
+      }
+    key = (uint64_t)best | ((uint64_t)sec << 32);
+  } else if constexpr (LAST) {
     // The last pass covers all N bins with cc == 0: bin = (l + T*gg) + MA*u.  Scanning
     // u-major / gg-minor visits the lane's bins in increasing order, so a strict '>'
     // keeps the lowest index among equal maxima (LoRaDetector.hpp:50-57).
@@ -480,7 +512,7 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
 // FFT of the symbol held as pass-1 inputs in z (T lanes x P points) and the lane's
 // argmax key.  KEEP: leave the spectrum in natural order in `row` (padded address
 // paddr(bin)) for the estimate's neighbour bins; NPASS == 1 keeps it in z.
-template <int SF, bool KEEP, bool FMA = false, bool TWL = false>
+template <int SF, bool KEEP, bool FMA = false, bool TWL = false, bool PACK = false>
 __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr,
                                             const cf* twl = nullptr) {
   using G = Geo<SF>;
@@ -516,14 +548,14 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
     // TWL: pass A's slot-major twiddles from the workgroup's LDS copy (k_demod_fast)
     const cf* twA = TWL ? twl : a.twTA;
     if constexpr (G::NPASS == 2) {
-      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA, false, TWL>(row, z, l, a.tw, key, twA, second);
+      pass_lds<G::RA, N, G::MA_A, SF, T, P, true, FMA, false, TWL, PACK>(row, z, l, a.tw, key, twA, second);
     } else {
       pass_lds<G::RA, N, G::MA_A, SF, T, P, false, FMA, false, TWL>(row, z, l, a.tw, key, twA);
       block_sync<WL>();
       write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
       block_sync<WL>();
       // TWL (speculative demod): pass B's twiddles two per 16-byte load (KArgs::twTB2)
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR, TWL>(
+      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR, TWL, PACK>(
           row, z, l, a.tw, key, ((TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
     }
     if constexpr (KEEP) {
@@ -635,6 +667,68 @@ __device__ __forceinline__ void group_reduce2(float& a, float& b, int tid, float
     for (int q = 1; q < WPS; ++q) {
       a = fmaxf(a, rf[2 * (wb + q)]);
       b = fmaxf(b, rf[2 * (wb + q) + 1]);
+    }
+  }
+}
+
+// Speculative demod: exchange with lane ^ o (o < 64) - DPP for o <= 8 (the values of a
+// reduction step are uniform over each aligned block of o lanes, so a mirror inside the
+// next block up is the same exchange), a lane permute beyond.
+template <int O>
+__device__ __forceinline__ uint32_t xchg_u32(uint32_t v) {
+  if constexpr (O == 1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  else if constexpr (O == 2)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  else if constexpr (O == 4)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  else if constexpr (O == 8)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  else
+    return (uint32_t)__shfl_xor((int)v, O, 64);
+}
+
+// (best, second) of the symbol's bins from every lane's (best, second) keys, and the max
+// of pm, over the symbol's T lanes (every lane gets them): the second is the runner-up of
+// the whole multiset of bins, so two lanes holding equal best keys give a zero margin.
+template <int O, int W>
+__device__ __forceinline__ void spec_reduce_step(uint32_t& best, uint32_t& sec, float& pm) {
+  if constexpr (O < W) {
+    const uint32_t ob = xchg_u32<O>(best), os = xchg_u32<O>(sec);
+    const float op = __uint_as_float(xchg_u32<O>(__float_as_uint(pm)));
+    const uint32_t lo = best < ob ? best : ob;
+    const uint32_t s2 = sec > os ? sec : os;
+    sec = s2 > lo ? s2 : lo;
+    best = best > ob ? best : ob;
+    pm = fmaxf(pm, op);
+    spec_reduce_step<2 * O, W>(best, sec, pm);
+  }
+}
+template <int SF>
+__device__ __forceinline__ void spec_reduce(uint32_t& best, uint32_t& sec, float& pm, int tid, uint32_t* scratch) {
+  constexpr int T = Geo<SF>::T;
+  spec_reduce_step<1, (T < 64 ? T : 64)>(best, sec, pm);
+  if constexpr (T > 64) {  // waves of one symbol: one LDS round (3 words per wave)
+    const int w = tid >> 6;
+    if ((tid & 63) == 0) {
+      scratch[3 * w] = best;
+      scratch[3 * w + 1] = sec;
+      scratch[3 * w + 2] = __float_as_uint(pm);
+    }
+    __syncthreads();
+    constexpr int WPS = T / 64;
+    const int wb = (w / WPS) * WPS;
+    best = scratch[3 * wb];
+    sec = scratch[3 * wb + 1];
+    pm = __uint_as_float(scratch[3 * wb + 2]);
+#pragma unroll
+    for (int q = 1; q < WPS; ++q) {
+      const uint32_t ob = scratch[3 * (wb + q)], os = scratch[3 * (wb + q) + 1];
+      const uint32_t lo = best < ob ? best : ob;
+      const uint32_t s2 = sec > os ? sec : os;
+      sec = s2 > lo ? s2 : lo;
+      best = best > ob ? best : ob;
+      pm = fmaxf(pm, __uint_as_float(scratch[3 * (wb + q) + 2]));
     }
   }
 }
@@ -804,24 +898,29 @@ __device__ __forceinline__ void stamp(int k, bool real) {
 // the symbol's index, its top-bin / runner-up margin and its window's max(|I|,|Q|) (one
 // 8-byte spec_marg store), certified or recomputed exactly by k_est_fast<SPEC = 2>.  The
 // arithmetic is k_demod_fast<SF, MODE, true, true>'s.
-// Persistent: a workgroup demodulates groups of SPW symbols blockIdx.x, blockIdx.x +
-// gstride, ... (gstride = the grid: a few workgroups per CU, launch_spec_demod).  Short
-// waves (about 4 us at SF7) left the CUs half occupied between one workgroup's end and the
-// next one's start; looping keeps every slot busy and stages the pass-A twiddles once.
+// Persistent: the work is cut into blocks of SPB consecutive data symbols of one frame
+// (a wave's 64/T symbols for T <= 64, the workgroup's SPW symbols beyond), so the frame,
+// its offsets and every address but the lane's own are wave-uniform (scalar registers
+// and scalar loads); a frame's last block may be partial.  A workgroup takes groups of BPG
+// blocks blockIdx.x, blockIdx.x + gstride, ... (gstride = the grid: a few workgroups per
+// CU, launch_spec_demod): short waves (about 4 us at SF7) left the CUs half occupied
+// between one workgroup's end and the next one's start.
 #ifndef LORA_SPEC_PERSIST
-#define LORA_SPEC_PERSIST 1
+#define LORA_SPEC_PERSIST 1  // 1: wave-local geometries (SF <= 10), 2: every SF, 0: none
 #endif
 template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
-LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t work, int rowc, int64_t gstride) {
+LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
   constexpr bool WL = G::WAVE_LOCAL;
+  constexpr int SPB = WL ? 64 / T : SPW;  // symbols per block
+  constexpr int BPG = WL ? 4 : 1;         // blocks per workgroup round
   constexpr int NTW = demod_twl_entries<SF, true>();
   static_assert(P == 16 && (MODE == 0 || MODE == 1), "SF >= 6, LEGACY osr 1");
   static_assert(NTW <= 256, "one staged twiddle per thread");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint64_t red[4];
+  __shared__ uint32_t red3[3 * 4];  // spec_reduce's cross-wave words (T > 64)
   cf* rows = reinterpret_cast<cf*>(smem);
   cf* twl = rows + (size_t)SPW * rowc;
   const int per = a.total - 2;
@@ -830,30 +929,29 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t work, int rowc, int64_t gstride) 
     if (tid < NTW) twl[tid] = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
     __syncthreads();
   }
-  const int64_t groups = (work + SPW - 1) / SPW;
+  const int bpf = (per + SPB - 1) / SPB;  // blocks per frame
+  const int64_t blocks = frames * bpf;
+  const int64_t groups = (blocks + BPG - 1) / BPG;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   typedef float v2f __attribute__((ext_vector_type(2)));
   int r = 0;
   for (int64_t grp = blockIdx.x; grp < groups; grp += gstride, ++r) {
-    // the lane index, opaque per group: left visible, the compiler hoists every lane
+    const int64_t b = grp * BPG + (WL ? wave : 0);  // wave-uniform
+    if (WL && b >= blocks) break;  // a wave-local wave leaves alone
+    // the lane index, opaque per round: left visible, the compiler hoists every lane
     // address out of the loop and keeps them live across it (more VGPRs, spills at SF12)
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    const int g = tid / T;  // slot
+    const int g = tid / T;  // slot in the workgroup (its LDS row)
     const int l = tid % T;  // lane within the symbol
     LORA_STAMP(5, true);
     LORA_STAMP(0, false);
-    // work item -> (frame, data symbol j): one 64-bit division per group (scalar unit),
-    // then a small per-lane quotient
-    const int64_t wb = grp * SPW;
-    const int64_t fb = wb / per;
-    const int rb = (int)(wb - fb * per);
-    const int64_t w = wb + g;
-    const bool valid = w < work;
-    const int loc = rb + (int)((valid ? w : work - 1) - wb);  // invalid lanes mirror a valid symbol
-    const int qf = per >= SPW ? (loc >= per ? 1 : 0) : (int)((unsigned)loc / (unsigned)per);
-    const int64_t f = fb + qf;
-    const int j = loc - qf * per;
-    const FrameParams& fp = a.fp_spec[f];
+    const int64_t f = b / bpf;
+    const int jb = (int)(b - f * bpf) * SPB;
+    const int jl = jb + (WL ? (g % SPB) : g);
+    const bool valid = jl < per;
+    const int j = valid ? jl : per - 1;  // a partial block's spare slots mirror a valid symbol
+    const FrameParams fp = a.fp_spec[f];
     const float rate = fp.rate;
     const int toff = fp.t_off;
     const int s = 2 + j;
@@ -890,20 +988,28 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t work, int rowc, int64_t gstride) 
     rotate_place<SF, true, true, true>(in, z, start, rate, false, a.win, l);
     asm volatile("" : "+v"(pm));
     LORA_STAMP(2, false);
-    float sec = 0.0f;
-    const uint64_t lkey = fft_key<SF, false, true, (NTW > 0)>(z, rows + (size_t)g * rowc, l, a, &sec, twl);
+    const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true>(z, rows + (size_t)g * rowc, l, a, nullptr, twl);
     LORA_STAMP(3, false);
-    const uint64_t key = symbol_key<SF>(lkey, tid, red);
-    // runner-up over the symbol: the top lane offers its own runner-up, the others their best
-    float r2 = lkey == key ? sec : key_value(lkey);
-    group_reduce2<SF>(r2, pm, tid, reinterpret_cast<float*>(smem + 64));
-    if (l == 0 && valid) {
-      if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)key_index(key);
-      reinterpret_cast<float2*>(a.spec_marg)[f * per + j] = make_float2(sqrtf(key_value(key)) - sqrtf(r2), pm);
+    // the symbol's best and runner-up keys over its lanes; the lane holding the best key
+    // stores the index (equal best keys in two lanes: a zero margin, so the certify kernel
+    // recomputes the symbol and overwrites it)
+    const uint32_t lbest = (uint32_t)lk;
+    uint32_t best = lbest, sec = (uint32_t)(lk >> 32);
+    spec_reduce<SF>(best, sec, pm, tid, red3);
+    if (valid) {
+      constexpr int NG = (G::NPASS == 2 ? P / G::RA : P / G::RB);
+      constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
+      if (lbest == best && a.syms) {
+        const int o = (int)(best & 15u);  // ordinal u * NG + gg: bin = l + T gg + ML u
+        a.syms[f * a.sym_stride + j] = (uint16_t)(l + T * (o % NG) + ML * (o / NG));
+      }
+      if (l == 0)
+        reinterpret_cast<float2*>(a.spec_marg)[f * per + j] =
+            make_float2(sqrtf(spec_key_value(best)) - sqrtf(spec_key_value(sec)), pm);
     }
     LORA_STAMP(4, false);
     LORA_STAMP(6, true);
-    block_sync<WL>();  // the rows (and group_reduce2's scratch) are rewritten by the next group
+    block_sync<WL>();  // the rows (and red3) are rewritten by the next round
   }
 }
 
@@ -1269,7 +1375,8 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     //    fract(fl(fl(r' T) fl(1/2pi))), T a power of two: within 2 u rmax T + 1.8e-7 of
     //    e^{i r' T}, and each product rounds by <= 2 sqrt2 u): e_spec = 5 u rmax L +
     //    u rmax N + 2 sqrt2 1.26e-7 + 15 (2 u rmax T + 1.8e-7 + 2 sqrt2 u) < 5 u rmax L +
-    //    u rmax N + 6e-6;
+    //    u rmax N + 6e-6; the demod ranks bins by keys that truncate |X|^2 by < 16 ulp
+    //    (spec_key), moving |X| by < 2^-20 |X|: e_spec = 5 u rmax L + u rmax N + 8e-6;
     //  * the two exact phases differ by |r - r'| L;
     //  * every other rounding (the product y * scale, the rotation product, log2 N
     //    butterfly stages with table twiddles, |X|^2 and its square root) moves a bin by
@@ -1299,7 +1406,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         const double n1 = 2.0 * N * (double)v.y;
         const double L = (double)(3 + j) * N + tabs;
         const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
-        const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 6e-6;
+        const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
         const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
         if (!(same_t && (double)v.x > 4.0 * B)) atomicOr(&fmask[g][j >> 6], 1ull << (j & 63));
       }
@@ -1338,61 +1445,31 @@ int row_complex() {
 }
 
 // ---- the speculative pipeline's estimate kernels, one lane group per symbol -----------
-// k_est_split<SF, MODE, SPEC>: stage 0 (SPEC 1, pre-pass) and stage 2 (SPEC 2, exact
-// estimate + certification) of the pipeline for LEGACY osr-1 unwindowed frames at SF 6-9
-// (2T <= 64 lanes per frame: a wave holds 64 / 2T frames).  The work and the arithmetic
-// are k_est_fast's; the layout differs: symbols 0 and 1 of a frame go to two lane groups
-// side by side (the offset estimate's two transforms and detector tails, then the two
-// sync symbols, run concurrently on different lanes instead of one after the other in
-// one group), and the certification spreads over both groups.  Twice the waves with half
-// the registers each: these kernels are latency-bound chains per frame.
+// k_est_split<SF, MODE>: stage 0 (the pre-pass) of the pipeline for LEGACY osr-1
+// unwindowed frames at SF 6-9 (2T <= 64 lanes per frame: a wave holds 64 / 2T frames).
+// The work and the arithmetic are k_est_fast<SF, MODE, 1>'s; the layout differs: symbols
+// 0 and 1 of a frame go to two lane groups side by side (the offset estimate's two
+// transforms and detector tails, then the two sync symbols, run concurrently on different
+// lanes instead of one after the other in one group).  Twice the waves with half the
+// registers each: the pre-pass is a latency-bound chain per frame (SF7: 13.7 vs 15-18 us).
+// The same split of stage 2 (exact estimate + certification) measured slower - 47.7 vs
+// 28-35 us, its certification state needs the registers - and was removed.
 #ifndef LORA_EST_SPLIT
 #define LORA_EST_SPLIT 1
 #endif
-// One data symbol s = 2 + j of frame f exactly as the reference computes it (scaled
-// samples, glibc-faithful rotation, kissfft order; LoRaDemod.cpp:137-175) by a T-lane
-// group, written to the output (k_est_split's recomputation of uncertified symbols).
 template <int SF, int MODE>
-__device__ __attribute__((noinline)) void recompute_symbol(const KArgs& a, const cf* __restrict__ x, int64_t f, int j,
-                                                          const FrameParams& q, cf* row, int l, bool valid) {
-  using G = Geo<SF>;
-  constexpr int N = G::N, T = G::T, P = G::P;
-  const int s = 2 + j;
-  int64_t base;
-  int cg;
-  sym_base(s, N, a.frame_len, q.t_off, base, cg);
-  const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off);
-  cf in[P], z[P];
-  gather_points<SF>(a, x + base, l, 1, N, cg, 1, MODE == 0, q.scaled ? q.scale : 1.0f, in);
-  rotate_place<SF, true>(in, z, start, q.rate, false, a.win, l);
-  uint64_t key = fft_key<SF, false>(z, row, l, a);
-  key = group_max(key, T);
-  if (l == 0 && valid) {
-    if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)key_index(key);
-    atomicAdd(a.spec_fix, 1u);
-  }
-  wave_sync();  // row is rewritten by the next transform
-}
-
-#ifndef LORA_EST_SPLIT_W2
-#define LORA_EST_SPLIT_W2 3  // waves per SIMD of the stage-2 kernel (the certification adds fp64 state)
-#endif
-template <int SF, int MODE, int SPEC>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SPEC == 1 ? 4 : LORA_EST_SPLIT_W2)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
 LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
+  [[maybe_unused]] constexpr int SPEC = 1;  // LORA_ESTAMP's stage
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
   constexpr int FPW = 64 / (2 * T);  // frames per wave (= block)
-  static_assert(SPEC == 1 || SPEC == 2, "pipeline stages 0 and 2");
   static_assert(2 * T <= 64 && P == 16, "SF 6-9");
   constexpr bool dech = MODE == 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ FrameParams sp[FPW];
   __shared__ float tail[FPW][2][4];  // per frame and symbol: index, fractional index, phase, -
   __shared__ uint32_t sws[FPW][2];
-  // SPEC 2: one bit per data symbol that failed certification (frames of up to
-  // kSpecChunks * T data symbols)
-  __shared__ unsigned long long fmask[SPEC == 2 ? FPW : 1][SPEC == 2 ? T : 1];
   const int tid = threadIdx.x;
   LORA_ESTAMP(5, true);
   LORA_ESTAMP(0, false);
@@ -1406,48 +1483,26 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
   const int64_t f = valid ? f0 : frames - 1;
   const cf* __restrict__ x = a.iq + f * a.frame_stride;
   cf* row = reinterpret_cast<cf*>(smem) + (size_t)g2 * rowc;
-  const int per = a.total - 2;
   // reduce over the frame's 2T lanes (the two groups of a frame are adjacent)
   auto frame_max = [&](float v) {
 #pragma unroll
     for (int o = T; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
   };
-  float maxv = 0.0f;
-  if constexpr (SPEC == 2) {
-    // LoRaDemod.cpp:59-67 from the pre-pass's slot (samples outside the data windows) and
-    // every data window's maximum (the demod's (margin, max) pairs)
-    maxv = __uint_as_float(a.maxbits[f]);
-    const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
-#pragma unroll 4
-    for (int j = l2; j < per; j += 2 * T) maxv = fmaxf(maxv, mg[j].y);
-    maxv = frame_max(maxv);
-  }
-  const int scaled = maxv > 1.0f;
-  const float scale = scaled ? 1.0f / maxv : 1.0f;
+  // the pre-pass works on the unscaled samples (LoRaDemod.cpp:59-77 comes later: the
+  // frame maximum is only known after the symbol pass)
+  const int scaled = 0;
+  const float scale = 1.0f;
   LORA_ESTAMP(1, false);
-  if (SPEC == 2 && !scaled && l2 == 0 && valid) {
-    // no rescaling: the pre-pass estimate and its sync word are the reference's
-    const FrameParams qs = a.fp_spec[f];
-    a.fp[f] = qs;
-    if (a.cfo) a.cfo[f] = qs.cfo;
-    if (a.toff) a.toff[f] = qs.toff;
-    if (a.max_amp) a.max_amp[f] = maxv;
-    if (a.sync) a.sync[f] = (uint8_t)qs.pad0;
-  }
   FrameParams q;
-  if (SPEC == 2 && !scaled) {
-    q = a.fp_spec[f];
-  } else {
+  {
     // LoRaDemod.cpp:79-123 (osr 1: one phase per symbol) for symbol `sym` of the frame
     cf in[P], z[P];
     gather_points<SF>(a, x + (int64_t)sym * N, l, 1, N, 0, 1, dech, scale, in);
-    float mo = 0.0f;  // SPEC 1: max(|I|,|Q|) over symbols 0/1 (this group's gathers)
-    if constexpr (SPEC == 1) {
+    float mo = 0.0f;  // max(|I|,|Q|) over symbols 0/1 (this group's gathers)
 #pragma unroll
-      for (int k = 0; k < P; ++k) mo = amax3(mo, in[k]);
-      asm volatile("" : "+v"(mo));
-    }
+    for (int k = 0; k < P; ++k) mo = amax3(mo, in[k]);
+    asm volatile("" : "+v"(mo));
     rotate_place<SF, false>(in, z, 0.0f, 0.0f, false, a.win, l);
     uint64_t key = fft_key<SF, true>(z, row, l, a);
     key = group_max(key, T);
@@ -1491,21 +1546,12 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
       qe.scaled = scaled;
       qe.pad0 = qe.pad1 = 0;
       sp[fg] = qe;
-      if (valid) {
-        if constexpr (SPEC == 1) {
-          a.fp_spec[f] = qe;
-        } else {
-          a.fp[f] = qe;
-          if (a.cfo) a.cfo[f] = cfo;
-          if (a.toff) a.toff[f] = toff;
-          if (a.max_amp) a.max_amp[f] = maxv;
-        }
-      }
+      if (valid) a.fp_spec[f] = qe;
     }
     wave_sync();
     q = sp[fg];
     LORA_ESTAMP(3, false);
-    if constexpr (SPEC == 1) {
+    {
       // the samples outside every data-symbol window of these offsets: [0, 2N) came with
       // the gathers above; a positive t_off's [2N, 2N + t_off) and the frame's tail here
       int64_t b2, bl;
@@ -1550,67 +1596,21 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
     if (l2 == 0 && valid) {
       const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
       const uint8_t word = (uint8_t)((((sws[fg][0] >> shift) & 0x0f) << 4) | ((sws[fg][1] >> shift) & 0x0f));
-      if constexpr (SPEC == 1)
-        a.fp_spec[f].pad0 = word;  // the pre-pass sync word, final when the frame is not rescaled
-      else if (a.sync)
-        a.sync[f] = word;
+      a.fp_spec[f].pad0 = word;  // the pre-pass sync word, final when the frame is not rescaled
     }
     LORA_ESTAMP(4, false);
-    if constexpr (SPEC == 1) {
-      LORA_ESTAMP(6, true);
-      return;
-    }
-  }
-  if constexpr (SPEC == 2) {
-    // certification of the data symbols (k_est_fast<SPEC = 2> states the bound)
-    const FrameParams qs = a.fp_spec[f];
-    const bool same_t = qs.t_off == q.t_off;
-    for (int w = l2; w < T; w += 2 * T) fmask[fg][w] = 0;
-    wave_sync();
-    {
-      const double u = 1.0 / 16777216.0;
-      const double E = (8.0 * SF + 32.0) * u;
-      const double drate = fabs((double)q.rate - (double)qs.rate);
-      const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
-      const double tabs = (double)abs(q.t_off);
-      const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
-#pragma unroll 1
-      for (int j = l2; j < per; j += 2 * T) {
-        const float2 v = mg[j];
-        const double n1 = 2.0 * N * (double)v.y;
-        const double L = (double)(3 + j) * N + tabs;
-        const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
-        const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 6e-6;
-        const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
-        if (!(same_t && (double)v.x > 4.0 * B)) atomicOr(&fmask[fg][j >> 6], 1ull << (j & 63));
-      }
-    }
-    wave_sync();
-    LORA_ESTAMP(7, false);
-    // recompute the failures exactly: the frame's two groups take turns (out of line: a
-    // rare path whose registers must not weigh on the rest of the kernel)
-    int k = 0;
-    for (int w = 0; w < (per + 63) >> 6; ++w) {
-      unsigned long long m = fmask[fg][w];
-      while (m) {
-        const int j = w * 64 + __builtin_ctzll(m);
-        m &= m - 1;
-        if ((k++ & 1) != sym) continue;  // group-uniform
-        recompute_symbol<SF, MODE>(a, x, f, j, q, row, l, valid);
-      }
-    }
     LORA_ESTAMP(6, true);
   }
 }
 
-template <int SF, int MODE, int SPEC>
+template <int SF, int MODE>
 bool launch_est_split(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
   constexpr int FPW = 64 / (2 * G::T);
   const int rowc = row_complex<SF>();
   const size_t lds = sizeof(cf) * (size_t)(2 * FPW) * rowc;
   const int64_t grid = (frames + FPW - 1) / FPW;
-  launch(k_est_split<SF, MODE, SPEC>, dim3((unsigned)grid), dim3(64), lds, st, a, frames, rowc);
+  launch(k_est_split<SF, MODE>, dim3((unsigned)grid), dim3(64), lds, st, a, frames, rowc);
   return true;
 }
 
@@ -1675,7 +1675,7 @@ int device_cus() {
 }
 
 template <int SF, int MODE>
-bool launch_spec_demod(const KArgs& a, int64_t work, hipStream_t st) {
+bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
   const size_t lds = sizeof(cf) * ((size_t)G::SPW * rowc + demod_twl_entries<SF, true>());
@@ -1684,10 +1684,15 @@ bool launch_spec_demod(const KArgs& a, int64_t work, hipStream_t st) {
     if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
       return false;
-  const int64_t groups = (work + G::SPW - 1) / G::SPW;
-  const int64_t cap = LORA_SPEC_PERSIST ? (int64_t)device_cus() * LORA_SPEC_WG_PER_CU : groups;
+  // the kernel's blocks: SPB symbols of one frame (see k_spec_demod), BPG per workgroup round
+  constexpr int SPB = G::WAVE_LOCAL ? 64 / G::T : G::SPW, BPG = G::WAVE_LOCAL ? 4 : 1;
+  const int per = a.total - 2;
+  const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB);
+  const int64_t groups = (blocks + BPG - 1) / BPG;
+  const bool persist = LORA_SPEC_PERSIST == 2 || (LORA_SPEC_PERSIST == 1 && G::WAVE_LOCAL);
+  const int64_t cap = persist ? (int64_t)device_cus() * LORA_SPEC_WG_PER_CU : groups;
   const int64_t grid = groups < cap ? groups : cap;
-  launch(k_spec_demod<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, work, rowc, grid);
+  launch(k_spec_demod<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
   return true;
 }
 
@@ -1697,14 +1702,12 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   if constexpr (SF < 6) {
     return false;
   } else {
-    const int64_t work = frames * (int64_t)(a.total - 2);
     if constexpr (SF <= 9 && LORA_EST_SPLIT) {
-      if (stage == 0)
-        return a.dechirp ? launch_est_split<SF, 0, 1>(a, frames, st) : launch_est_split<SF, 1, 1>(a, frames, st);
+      if (stage == 0) return a.dechirp ? launch_est_split<SF, 0>(a, frames, st) : launch_est_split<SF, 1>(a, frames, st);
     }
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
     if (stage == 1)
-      return a.dechirp ? launch_spec_demod<SF, 0>(a, work, st) : launch_spec_demod<SF, 1>(a, work, st);
+      return a.dechirp ? launch_spec_demod<SF, 0>(a, frames, st) : launch_spec_demod<SF, 1>(a, frames, st);
     return a.dechirp ? launch_est_mode<SF, 0, 2>(a, frames, st) : launch_est_mode<SF, 1, 2>(a, frames, st);
   }
 }
