@@ -942,8 +942,8 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     // address out of the loop and keeps them live across it (more VGPRs, spills at SF12)
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    const int g = tid / T;  // slot in the workgroup (its LDS row)
-    const int l = tid % T;  // lane within the symbol
+    const int g = SPW == 1 ? 0 : tid / T;  // slot in the workgroup (its LDS row)
+    const int l = tid % T;                 // lane within the symbol
     LORA_STAMP(5, true);
     LORA_STAMP(0, false);
     const int64_t f = b / bpf;
@@ -958,23 +958,29 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     int64_t base;
     int cg;
     sym_base(s, N, a.frame_len, toff, base, cg);
-    // the window's samples (read once: nontemporal) and the dechirp table pairs
+    // the window's samples (read once: nontemporal) and the dechirp table pairs, through
+    // buffer resources on wave-uniform bases (the frame, the table): the point offsets T q
+    // (up to 30 KB at SF12) go in the scalar offset or the immediate, not in 64-bit vector
+    // adds.  Byte offsets fit 31 bits: the pipeline's frames hold < 2^26 samples.
     cf in[P];
     {
-      const v2f* __restrict__ xl = reinterpret_cast<const v2f*>(a.iq + f * a.frame_stride + base + l);
+      const __amdgpu_buffer_rsrc_t rx =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + f * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
+      const int vo = (int)(base + l) * 8;
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-        const v2f v = __builtin_nontemporal_load(xl + T * q);
+        const v2f v = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
         in[q] = cf{v.x, v.y};
       }
     }
     // caller-side dechirp (e2e_chain_test.cpp:88-93) with the reference's products, the
     // window's max(|I|,|Q|) of exactly these samples, then the rotation
     if constexpr (MODE == 0) {
-      const float4* __restrict__ dp = reinterpret_cast<const float4*>(a.downP) + cg + l;
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
+      const int vo = (cg + l) * 16;
 #pragma unroll
       for (int pp = 0; pp < P / 2; ++pp) {
-        const float4 d = dp[pp * (N + T)];
+        const float4 d = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vo, pp * (N + T) * 16, 0));
         in[2 * pp] = cmul(in[2 * pp], cf{d.x, d.y});
         in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{d.z, d.w});
       }

@@ -18,7 +18,7 @@ namespace lora {
 // float(M_PI), the reference's `float(M_PI)` (phy.cpp:40, LoRaDemod.cpp)
 constexpr float PI_F = 3.14159265358979323846f;
 
-struct cf {
+struct alignas(8) cf {  // 8-byte aligned: one 64-bit LDS / global access per value
   float re, im;
 };
 
