@@ -908,6 +908,9 @@ __device__ __forceinline__ void stamp(int k, bool real) {
 #ifndef LORA_SPEC_PERSIST
 #define LORA_SPEC_PERSIST 1  // 1: wave-local geometries (SF <= 10), 2: every SF, 0: none
 #endif
+#ifndef LORA_SPEC_PREFETCH
+#define LORA_SPEC_PREFETCH 0
+#endif
 template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
@@ -934,10 +937,57 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   const int64_t groups = (blocks + BPG - 1) / BPG;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   typedef float v2f __attribute__((ext_vector_type(2)));
-  int r = 0;
-  for (int64_t grp = blockIdx.x; grp < groups; grp += gstride, ++r) {
-    const int64_t b = grp * BPG + (WL ? wave : 0);  // wave-uniform
-    if (WL && b >= blocks) break;  // a wave-local wave leaves alone
+  // block b (wave-uniform) -> frame f, the lane's data symbol j and its window
+  struct Loc {
+    int64_t f, base;
+    int j, cg, toff;
+    float rate;
+    bool valid;
+  };
+  auto locate = [&](int64_t b, int g) {
+    Loc L;
+    L.f = b / bpf;
+    const int jl = (int)(b - L.f * bpf) * SPB + (WL ? (g % SPB) : g);
+    L.valid = jl < per;
+    L.j = L.valid ? jl : per - 1;  // a partial block's spare slots mirror a valid symbol
+    const FrameParams fp = a.fp_spec[L.f];
+    L.rate = fp.rate;
+    L.toff = fp.t_off;
+    sym_base(2 + L.j, N, a.frame_len, L.toff, L.base, L.cg);
+    return L;
+  };
+  // the window's samples (read once: nontemporal) through a buffer resource on the
+  // wave-uniform frame base: the point offsets T q (up to 30 KB at SF12) go in the scalar
+  // offset or the immediate, not in 64-bit vector adds.  Byte offsets fit 31 bits: the
+  // pipeline's frames hold < 2^26 samples.
+  auto load_iq = [&](const Loc& L, int l, cf* dst) {
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + L.f * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
+    const int vo = (int)(L.base + l) * 8;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const v2f v = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
+      dst[q] = cf{v.x, v.y};
+    }
+  };
+  // PF: the next round's samples are requested during this round (its table values first:
+  // loads complete in order, so a table load issued after the prefetch would wait for it).
+  // Only where no vector load follows inside the transform (two-pass geometries, SF <= 8).
+  constexpr bool PF = LORA_SPEC_PREFETCH && G::NPASS == 2;
+  int64_t grp = blockIdx.x;
+  int64_t b = grp * BPG + (WL ? wave : 0);  // wave-uniform
+  bool have = grp < groups && (!WL || b < blocks);
+  cf nx[PF ? P : 1];
+  Loc nl{};
+  if constexpr (PF) {
+    if (have) {
+      const int tid = threadIdx.x;
+      nl = locate(b, SPW == 1 ? 0 : tid / T);
+      load_iq(nl, tid % T, nx);
+    }
+  }
+  for (int r = 0; have; ++r) {
+    (void)r;  // the round (diagnostic stamps of the first one)
     // the lane index, opaque per round: left visible, the compiler hoists every lane
     // address out of the loop and keeps them live across it (more VGPRs, spills at SF12)
     int tid = threadIdx.x;
@@ -946,43 +996,46 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     const int l = tid % T;                 // lane within the symbol
     LORA_STAMP(5, true);
     LORA_STAMP(0, false);
-    const int64_t f = b / bpf;
-    const int jb = (int)(b - f * bpf) * SPB;
-    const int jl = jb + (WL ? (g % SPB) : g);
-    const bool valid = jl < per;
-    const int j = valid ? jl : per - 1;  // a partial block's spare slots mirror a valid symbol
-    const FrameParams fp = a.fp_spec[f];
-    const float rate = fp.rate;
-    const int toff = fp.t_off;
-    const int s = 2 + j;
-    int64_t base;
-    int cg;
-    sym_base(s, N, a.frame_len, toff, base, cg);
-    // the window's samples (read once: nontemporal) and the dechirp table pairs, through
-    // buffer resources on wave-uniform bases (the frame, the table): the point offsets T q
-    // (up to 30 KB at SF12) go in the scalar offset or the immediate, not in 64-bit vector
-    // adds.  Byte offsets fit 31 bits: the pipeline's frames hold < 2^26 samples.
+    const Loc L = PF ? nl : locate(b, g);
+    const int64_t f = L.f;
+    const int j = L.j, s = 2 + L.j, toff = L.toff;
+    const bool valid = L.valid;
+    const float rate = L.rate;
     cf in[P];
-    {
-      const __amdgpu_buffer_rsrc_t rx =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + f * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
-      const int vo = (int)(base + l) * 8;
+    if constexpr (PF) {
 #pragma unroll
-      for (int q = 0; q < P; ++q) {
-        const v2f v = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
-        in[q] = cf{v.x, v.y};
+      for (int q = 0; q < P; ++q) in[q] = nx[q];
+    } else {
+      load_iq(L, l, in);
+    }
+    // the caller-side dechirp's table pairs (two values per 16-byte load)
+    float4 dt[MODE == 0 ? P / 2 : 1];
+    if constexpr (MODE == 0) {
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
+      const int vo = (L.cg + l) * 16;
+#pragma unroll
+      for (int pp = 0; pp < P / 2; ++pp)
+        dt[pp] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vo, pp * (N + T) * 16, 0));
+    }
+    // the next round
+    grp += gstride;
+    b = grp * BPG + (WL ? wave : 0);
+    have = grp < groups && (!WL || b < blocks);
+    if constexpr (PF) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (have) {
+        nl = locate(b, g);
+        load_iq(nl, l, nx);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     // caller-side dechirp (e2e_chain_test.cpp:88-93) with the reference's products, the
     // window's max(|I|,|Q|) of exactly these samples, then the rotation
     if constexpr (MODE == 0) {
-      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
-      const int vo = (cg + l) * 16;
 #pragma unroll
       for (int pp = 0; pp < P / 2; ++pp) {
-        const float4 d = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vo, pp * (N + T) * 16, 0));
-        in[2 * pp] = cmul(in[2 * pp], cf{d.x, d.y});
-        in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{d.z, d.w});
+        in[2 * pp] = cmul(in[2 * pp], cf{dt[pp].x, dt[pp].y});
+        in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
       }
     }
     float pm = 0.0f;
