@@ -1103,8 +1103,49 @@ struct EstGeo {
 // estimate, its outputs and sync word, then the certification of every data symbol the
 // demod computed from unscaled samples with the pre-pass offsets: a symbol whose argmax
 // margin exceeds the rounding bound keeps its index, any other is recomputed exactly here.
+// Lane 0's scalar tails of the offset estimate, out of line (their libm registers would
+// otherwise count against every lane of the latency-bound estimate kernels).
+__device__ __attribute__((noinline)) void est_tail(float fund2, cf L, cf R, float power_scale, float* pw, float* fi) {
+  detect_tail(fund2, L, R, power_scale, pw, fi);
+}
+__device__ __attribute__((noinline)) float est_phase(cf b) { return lm_atan2f(b.im, b.re); }
+
+// One symbol s of the frame at x exactly as the reference computes it with the offsets q
+// (scaled samples, glibc-faithful rotation, kissfft order; LoRaDemod.cpp:137-175,
+// phy.cpp:209-237): its argmax index, on every lane of the group.  Out of line: the
+// estimate kernels call it for the sync symbols and for data symbols the speculative
+// demod could not certify, short or rare paths whose registers (the exact sincosf) must
+// not weigh on the estimate's transforms.
+template <int SF, int MODE>
+__device__ __attribute__((noinline)) uint32_t exact_symbol(const KArgs& a, const cf* __restrict__ x,
+                                                           const FrameParams& q, int s, cf* row, int l, int tid,
+                                                           uint64_t* red) {
+  using G = Geo<SF>;
+  constexpr int N = G::N, P = G::P;
+  constexpr bool DYN = MODE == 2;
+  const int step = DYN ? a.step : N;
+  const int osr = DYN ? a.osr : 1;
+  const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
+  const bool dech = DYN ? (legacy && a.dechirp) : (MODE == 0);
+  const bool hann = DYN ? (a.hann != 0) : false;
+  int64_t base;
+  int cg;
+  sym_base(s, step, a.frame_len, q.t_off, base, cg);
+  const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
+  cf in[P], z[P];
+  gather_points<SF>(a, x + base, l, osr, step, cg, legacy ? 1 : 2, dech, (legacy && q.scaled) ? q.scale : 1.0f, in);
+  rotate_place<SF, true>(in, z, start, q.rate, hann, a.win, l);
+  uint64_t key = fft_key<SF, false>(z, row, l, a);
+  key = symbol_key<SF>(key, tid, red);
+  block_sync<G::WAVE_LOCAL>();  // the row (and red) are rewritten by the next transform
+  return key_index(key);
+}
+
+#ifndef LORA_EST_WAVES
+#define LORA_EST_WAVES 2
+#endif
 template <int SF, int MODE, int SPEC = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EstGeo<SF>::PAIR ? 2 : LORA_EST_WAVES)))
 LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
@@ -1275,7 +1316,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
             B = row[lds_slot<SF>((int)idx)];
           }
           float pw, fi;
-          detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
+          est_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
           if (pw > best_p || (legacy && pw == best_p && idx < best_idx)) {
             best_p = pw;
             best_idx = idx;
@@ -1289,7 +1330,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       if (l == 0) {
         sum_t += best_t;
         sum_index += (float)best_idx + best_fi;
-        const float phase = lm_atan2f(best_bin.im, best_bin.re);
+        const float phase = est_phase(best_bin);
         if (have_prev) {
           float d = phase - prev_phase;
           while (d > PI_F) d -= 2.0f * PI_F;
@@ -1387,19 +1428,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       sw[0] = key_index(group_max(k0, T));
       sw[1] = key_index(group_max(k1, T));
     }
-    for (int s = 0; s < (PAIR ? 0 : 2); ++s) {
-      int64_t base;
-      int cg;
-      sym_base(s, step, a.frame_len, q.t_off, base, cg);
-      const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
-      gather_points<SF>(a, x + base, l, osr, step, cg, legacy ? 1 : 2, dech,
-                           (legacy && q.scaled) ? q.scale : 1.0f, in);
-      rotate_place<SF, true>(in, z, start, q.rate, hann, a.win, l);
-      uint64_t key = fft_key<SF, false>(z, row, l, a);
-      key = symbol_key<SF>(key, tid, red);
-      sw[s] = key_index(key);
-      block_sync<G::WAVE_LOCAL>();
-    }
+    for (int s = 0; s < (PAIR ? 0 : 2); ++s) sw[s] = exact_symbol<SF, MODE>(a, x, q, s, row, l, tid, red);
     if (l == 0 && valid) {
       const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
       const uint8_t word = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
@@ -1472,26 +1501,16 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     }
     block_sync<G::WAVE_LOCAL>();
     LORA_ESTAMP(7, false);
-    cf in[P], z[P];
     for (int w = 0; w < (per + 63) >> 6; ++w) {  // group-uniform: every lane reads the same words
       unsigned long long m = fmask[g][w];
       while (m) {
         const int j = w * 64 + __builtin_ctzll(m);
         m &= m - 1;
-        const int s = 2 + j;
-        int64_t base;
-        int cg;
-        sym_base(s, step, a.frame_len, q.t_off, base, cg);
-        const float start = q.rate * ((float)((uint32_t)s * (uint32_t)N) + (float)q.t_off / (float)osr);
-        gather_points<SF>(a, x + base, l, osr, step, cg, 1, dech, q.scaled ? q.scale : 1.0f, in);
-        rotate_place<SF, true>(in, z, start, q.rate, hann, a.win, l);
-        uint64_t key = fft_key<SF, false>(z, row, l, a);
-        key = symbol_key<SF>(key, tid, red);
+        const uint32_t idx = exact_symbol<SF, MODE>(a, x, q, 2 + j, row, l, tid, red);
         if (l == 0 && valid) {
-          if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)key_index(key);
+          if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)idx;
           atomicAdd(a.spec_fix, 1u);
         }
-        block_sync<G::WAVE_LOCAL>();  // row is rewritten by the next transform
       }
     }
     LORA_ESTAMP(6, true);
