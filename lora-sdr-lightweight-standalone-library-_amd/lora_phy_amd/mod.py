@@ -1,6 +1,8 @@
 """GPU modulation: lora_mod_batch wrapper and the LoRaMod block."""
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 
 from . import _capi
@@ -8,11 +10,12 @@ from .demod import _require_cuda, _stream_handle
 
 
 def modulate(symbols: torch.Tensor, sf: int, osr: int = 1, bw: int = 125000,
-             amplitude: float = 1.0, sync: int = 0x12) -> torch.Tensor:
+             amplitude: float = 1.0, sync: int = 0x12, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """lora_modulate (LoRaMod.cpp:8-43) for a [F, S] (or [S]) uint16/int CUDA tensor.
 
     Returns complex64 [F, (S+2)*N*osr] (or 1-D): two sync up-chirps, then one
-    up-chirp per symbol, phase-continuous within each frame.
+    up-chirp per symbol, phase-continuous within each frame.  `out`: a contiguous
+    complex64 tensor of that shape on the symbols' device to write into (no allocation).
     """
     _require_cuda(symbols, "symbols")
     squeeze = symbols.dim() == 1
@@ -23,7 +26,14 @@ def modulate(symbols: torch.Tensor, sf: int, osr: int = 1, bw: int = 125000,
     F, S = s.shape
     osr = int(osr) if osr else 1
     per = (S + 2) * (1 << int(sf)) * osr
-    out = torch.empty((F, per), dtype=torch.complex64, device=s.device)
+    if out is None:
+        out = torch.empty((F, per), dtype=torch.complex64, device=s.device)
+    else:
+        want = (per,) if squeeze else (F, per)
+        if (tuple(out.shape) != want or out.dtype != torch.complex64 or out.device != s.device
+                or not out.is_contiguous()):
+            raise ValueError(f"out must be a contiguous complex64 {want} tensor on {s.device}")
+        out = out.view(F, per)
     lib = _capi.lib()
     _capi.check(lib.lora_mod_batch(int(sf), osr, int(bw), float(amplitude), int(sync) & 0xFF,
                                    s.data_ptr() if S > 0 else None, F, S, out.data_ptr(),

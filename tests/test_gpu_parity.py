@@ -166,6 +166,19 @@ def test_modulator_matches_oracle(O, amd, sf, osr, bw):
         np.testing.assert_array_equal(got[f].view(np.uint32), ref.view(np.uint32))
 
 
+def test_modulator_into_a_preallocated_buffer(amd):
+    """modulate(..., out=): the same samples written into the caller's buffer (what
+    bench.py times), and a wrong-shaped buffer is refused."""
+    syms = torch.randint(0, 128, (3, 9), dtype=torch.int32).cuda()
+    ref = amd.modulate(syms, 7)
+    out = torch.full_like(ref, complex(7.0, 7.0))
+    got = amd.modulate(syms, 7, out=out)
+    assert got.data_ptr() == out.data_ptr()
+    assert torch.equal(out.view(torch.int64), ref.view(torch.int64))
+    with pytest.raises(ValueError):
+        amd.modulate(syms, 7, out=torch.empty((3, 10), dtype=torch.complex64, device="cuda"))
+
+
 def test_estimate_and_compensate_match_oracle(O, amd):
     rng = np.random.default_rng(5)
     sf, osr = 8, 2
