@@ -16,16 +16,21 @@
 //     packet's completion signal.  Packets, kernel arguments and the signal are memory
 //     set up once in aql_create; kernel objects are looked up once per kernel.
 //
-// Kernel objects come from the code object the HIP runtime already loaded for this
-// library (the drop-in's init runs its warm-up frames through HIP first): the device
-// symbol name from hipKernelNameRefByPtr, the executable from the HSA loader extension.
+// Kernel objects: aql_create loads this library's own gfx950 code objects (the clang
+// offload bundles in its .hip_fatbin section, read from the file dladdr names) into HSA
+// executables on the device's agent; a kernel's symbol is found by the device name
+// hipKernelNameRefByPtr gives for its host stub.  The HIP runtime keeps its own copy for
+// every other call.
+#include <dlfcn.h>
+#include <elf.h>
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
-#include <hsa/hsa_ven_amd_loader.h>
 
+#include <cstdio>
 #include <cstring>
 #include <ctime>
+#include <vector>
 
 #include "lora_internal.h"
 
@@ -35,6 +40,7 @@ namespace {
 
 constexpr unsigned kSlotBytes = 1024;  // kernarg slot per packet (explicit + 256 hidden)
 constexpr int kCache = 32;
+constexpr int kMaxExec = 8;
 
 struct AqlKernel {
   const void* fn;
@@ -49,7 +55,8 @@ struct AqlQueue {
   hsa_queue_t* q = nullptr;
   hsa_signal_t done{};
   unsigned char* kernarg = nullptr;
-  hsa_ven_amd_loader_1_03_pfn_t loader{};
+  hsa_executable_t exec[kMaxExec]{};
+  int nexec = 0;
   AqlKernel k[kCache];
   int nk = 0;
   bool hsa_up = false;
@@ -110,58 +117,92 @@ hsa_status_t find_cpu_pool(hsa_agent_t a, void* data) {
   return static_cast<PoolFind*>(data)->found ? HSA_STATUS_INFO_BREAK : HSA_STATUS_SUCCESS;
 }
 
-struct SymFind {
-  const char* name;
-  hsa_agent_t agent;
-  hsa_executable_symbol_t sym{};
-  bool found = false;
-};
-
-hsa_status_t find_symbol(hsa_executable_t e, void* data) {
-  SymFind* f = static_cast<SymFind*>(data);
-  hsa_agent_t ag = f->agent;
-  if (hsa_executable_get_symbol_by_name(e, f->name, &ag, &f->sym) == HSA_STATUS_SUCCESS) {
-    f->found = true;
-    return HSA_STATUS_INFO_BREAK;
-  }
-  return HSA_STATUS_SUCCESS;
-}
-
 const AqlKernel* kernel_of(AqlQueue* Q, const void* fn) {
   for (int i = 0; i < Q->nk; ++i)
     if (Q->k[i].fn == fn) return &Q->k[i];
   if (Q->nk == kCache) return nullptr;
-  // first use of this kernel: its device name, then the symbol in a loaded executable
+  // first use of this kernel: its device name, then the symbol in one of the executables
   const char* name = hipKernelNameRefByPtr(fn, nullptr);
   if (!name) return nullptr;
   char buf[512];
   const size_t len = std::strlen(name);
   if (len + 4 > sizeof(buf)) return nullptr;
-  SymFind f{name, Q->agent};
-  Q->loader.hsa_ven_amd_loader_iterate_executables(find_symbol, &f);
-  if (!f.found) {  // kernel descriptors are also listed under "<name>.kd"
-    std::memcpy(buf, name, len);
-    std::memcpy(buf + len, ".kd", 4);
-    f.name = buf;
-    Q->loader.hsa_ven_amd_loader_iterate_executables(find_symbol, &f);
-  }
-  if (!f.found) return nullptr;
-  hsa_symbol_kind_t kind;
-  if (hsa_executable_symbol_get_info(f.sym, HSA_EXECUTABLE_SYMBOL_INFO_TYPE, &kind) != HSA_STATUS_SUCCESS ||
-      kind != HSA_SYMBOL_KIND_KERNEL)
-    return nullptr;
+  std::memcpy(buf, name, len);
+  std::memcpy(buf + len, ".kd", 4);
+  hsa_executable_symbol_t sym{};
+  bool found = false;
+  for (int e = 0; e < Q->nexec && !found; ++e)
+    for (const char* nm : {name, (const char*)buf}) {  // the kernel, or its descriptor's name
+      hsa_agent_t ag = Q->agent;
+      hsa_symbol_kind_t kind;
+      if (hsa_executable_get_symbol_by_name(Q->exec[e], nm, &ag, &sym) == HSA_STATUS_SUCCESS &&
+          hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_TYPE, &kind) == HSA_STATUS_SUCCESS &&
+          kind == HSA_SYMBOL_KIND_KERNEL) {
+        found = true;
+        break;
+      }
+    }
+  if (!found) return nullptr;
   AqlKernel k{fn, 0, 0, 0, 0};
-  if (hsa_executable_symbol_get_info(f.sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.object) !=
+  if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.object) !=
           HSA_STATUS_SUCCESS ||
-      hsa_executable_symbol_get_info(f.sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kernarg) !=
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kernarg) !=
           HSA_STATUS_SUCCESS ||
-      hsa_executable_symbol_get_info(f.sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.group) !=
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.group) !=
           HSA_STATUS_SUCCESS ||
-      hsa_executable_symbol_get_info(f.sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.priv) !=
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.priv) !=
           HSA_STATUS_SUCCESS)
     return nullptr;
   Q->k[Q->nk] = k;
   return &Q->k[Q->nk++];
+}
+
+// The gfx950 code objects of the clang offload bundles in this library's .hip_fatbin
+// section (uncompressed bundles: "__CLANG_OFFLOAD_BUNDLE__", an entry count, then per
+// entry offset, size, triple length and triple).
+bool own_code_objects(std::vector<unsigned char>& file, std::vector<std::pair<size_t, size_t>>& objs) {
+  Dl_info info{};
+  if (!dladdr(reinterpret_cast<void*>(&aql_create), &info) || !info.dli_fname) return false;
+  FILE* fp = std::fopen(info.dli_fname, "rb");
+  if (!fp) return false;
+  std::fseek(fp, 0, SEEK_END);
+  const long n = std::ftell(fp);
+  std::fseek(fp, 0, SEEK_SET);
+  file.resize(n > 0 ? (size_t)n : 0);
+  const bool ok = n > 0 && std::fread(file.data(), 1, file.size(), fp) == file.size();
+  std::fclose(fp);
+  if (!ok || file.size() < sizeof(Elf64_Ehdr)) return false;
+  const Elf64_Ehdr* eh = reinterpret_cast<const Elf64_Ehdr*>(file.data());
+  if (std::memcmp(eh->e_ident, ELFMAG, SELFMAG) != 0 || eh->e_shoff == 0 ||
+      eh->e_shoff + (size_t)eh->e_shnum * sizeof(Elf64_Shdr) > file.size() || eh->e_shstrndx >= eh->e_shnum)
+    return false;
+  const Elf64_Shdr* sh = reinterpret_cast<const Elf64_Shdr*>(file.data() + eh->e_shoff);
+  const Elf64_Shdr& strs = sh[eh->e_shstrndx];
+  for (int i = 0; i < eh->e_shnum; ++i) {
+    if (sh[i].sh_name >= strs.sh_size) continue;
+    const char* nm = reinterpret_cast<const char*>(file.data() + strs.sh_offset + sh[i].sh_name);
+    if (std::strcmp(nm, ".hip_fatbin") != 0 || sh[i].sh_offset + sh[i].sh_size > file.size()) continue;
+    static const char kMagic[] = "__CLANG_OFFLOAD_BUNDLE__";
+    const size_t lo = sh[i].sh_offset, hi = lo + sh[i].sh_size;
+    for (size_t pos = lo; pos + 32 <= hi; pos += 8) {  // bundles start 8-byte aligned
+      if (std::memcmp(file.data() + pos, kMagic, 24) != 0) continue;
+      uint64_t cnt;
+      std::memcpy(&cnt, file.data() + pos + 24, 8);
+      size_t p = pos + 32;
+      for (uint64_t e = 0; e < cnt && p + 24 <= hi; ++e) {
+        uint64_t off, size, tlen;
+        std::memcpy(&off, file.data() + p, 8);
+        std::memcpy(&size, file.data() + p + 8, 8);
+        std::memcpy(&tlen, file.data() + p + 16, 8);
+        if (p + 24 + tlen > hi) break;
+        const std::string triple(reinterpret_cast<const char*>(file.data() + p + 24), tlen);
+        p += 24 + tlen;
+        if (triple.find("gfx950") != std::string::npos && pos + off + size <= hi)
+          objs.emplace_back(pos + off, (size_t)size);
+      }
+    }
+  }
+  return !objs.empty();
 }
 
 double now_s() {
@@ -187,19 +228,6 @@ int aql_create(int device, AqlQueue** out) {
   Q->hsa_up = true;
   int rc = 0;
   do {
-    bool ext = false;
-    uint16_t minor = 0;
-    if (hsa_system_major_extension_supported(HSA_EXTENSION_AMD_LOADER, 1, &minor, &ext) != HSA_STATUS_SUCCESS ||
-        !ext || minor < 3) {  // iterate_executables arrived with 1.03
-      rc = -103;
-      break;
-    }
-    if (hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof(Q->loader), &Q->loader) !=
-            HSA_STATUS_SUCCESS ||
-        !Q->loader.hsa_ven_amd_loader_iterate_executables) {
-      rc = -104;
-      break;
-    }
     // HSA_AMD_AGENT_INFO_BDFID: bus << 8 | device << 3 | function
     AgentFind af{(uint32_t)(((bus & 0xff) << 8) | ((dev & 0x1f) << 3)), (uint32_t)dom};
     hsa_iterate_agents(find_gpu, &af);
@@ -239,6 +267,36 @@ int aql_create(int device, AqlQueue** out) {
       rc = -110;
       break;
     }
+    // this library's gfx950 code objects, loaded for the agent
+    std::vector<unsigned char> file;
+    std::vector<std::pair<size_t, size_t>> objs;
+    if (!own_code_objects(file, objs) || objs.size() > (size_t)kMaxExec) {
+      rc = -103;
+      break;
+    }
+    for (const auto& o : objs) {
+      hsa_code_object_reader_t rd{};
+      hsa_executable_t ex{};
+      if (hsa_code_object_reader_create_from_memory(file.data() + o.first, o.second, &rd) != HSA_STATUS_SUCCESS) {
+        rc = -104;
+        break;
+      }
+      if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &ex) !=
+          HSA_STATUS_SUCCESS) {
+        hsa_code_object_reader_destroy(rd);
+        rc = -104;
+        break;
+      }
+      Q->exec[Q->nexec++] = ex;
+      const bool loaded = hsa_executable_load_agent_code_object(ex, Q->agent, rd, nullptr, nullptr) ==
+                              HSA_STATUS_SUCCESS &&
+                          hsa_executable_freeze(ex, nullptr) == HSA_STATUS_SUCCESS;
+      hsa_code_object_reader_destroy(rd);  // loaded code does not depend on the reader
+      if (!loaded) {
+        rc = -104;
+        break;
+      }
+    }
   } while (false);
   if (rc != 0) {
     aql_destroy(Q);
@@ -253,6 +311,7 @@ void aql_destroy(AqlQueue* Q) {
   if (Q->done.handle) hsa_signal_destroy(Q->done);
   if (Q->q) hsa_queue_destroy(Q->q);
   if (Q->kernarg) hsa_amd_memory_pool_free(Q->kernarg);
+  for (int e = 0; e < Q->nexec; ++e) hsa_executable_destroy(Q->exec[e]);
   if (Q->hsa_up) hsa_shut_down();
   delete Q;
 }

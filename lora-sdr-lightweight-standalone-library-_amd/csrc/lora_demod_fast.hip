@@ -1103,21 +1103,14 @@ struct EstGeo {
 // estimate, its outputs and sync word, then the certification of every data symbol the
 // demod computed from unscaled samples with the pre-pass offsets: a symbol whose argmax
 // margin exceeds the rounding bound keeps its index, any other is recomputed exactly here.
-// Lane 0's scalar tails of the offset estimate, out of line (their libm registers would
-// otherwise count against every lane of the latency-bound estimate kernels).
-__device__ __attribute__((noinline)) void est_tail(float fund2, cf L, cf R, float power_scale, float* pw, float* fi) {
-  detect_tail(fund2, L, R, power_scale, pw, fi);
-}
-__device__ __attribute__((noinline)) float est_phase(cf b) { return lm_atan2f(b.im, b.re); }
-
 // One symbol s of the frame at x exactly as the reference computes it with the offsets q
 // (scaled samples, glibc-faithful rotation, kissfft order; LoRaDemod.cpp:137-175,
-// phy.cpp:209-237): its argmax index, on every lane of the group.  Out of line: the
-// estimate kernels call it for the sync symbols and for data symbols the speculative
-// demod could not certify, short or rare paths whose registers (the exact sincosf) must
-// not weigh on the estimate's transforms.
+// phy.cpp:209-237): its argmax index, on every lane of the group - the estimate kernels'
+// sync symbols and the data symbols the speculative demod could not certify.  (Out of
+// line it cut the SF12 pre-pass from 248 to 180 VGPRs but the calls' register saves made
+// the SF12 step 0.8-1.2 ms slower at 2-4 waves per SIMD; inlined.)
 template <int SF, int MODE>
-__device__ __attribute__((noinline)) uint32_t exact_symbol(const KArgs& a, const cf* __restrict__ x,
+__device__ __forceinline__ uint32_t exact_symbol(const KArgs& a, const cf* __restrict__ x,
                                                            const FrameParams& q, int s, cf* row, int l, int tid,
                                                            uint64_t* red) {
   using G = Geo<SF>;
@@ -1316,7 +1309,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
             B = row[lds_slot<SF>((int)idx)];
           }
           float pw, fi;
-          est_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
+          detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
           if (pw > best_p || (legacy && pw == best_p && idx < best_idx)) {
             best_p = pw;
             best_idx = idx;
@@ -1330,7 +1323,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       if (l == 0) {
         sum_t += best_t;
         sum_index += (float)best_idx + best_fi;
-        const float phase = est_phase(best_bin);
+        const float phase = lm_atan2f(best_bin.im, best_bin.re);
         if (have_prev) {
           float d = phase - prev_phase;
           while (d > PI_F) d -= 2.0f * PI_F;
@@ -1428,7 +1421,10 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       sw[0] = key_index(group_max(k0, T));
       sw[1] = key_index(group_max(k1, T));
     }
-    for (int s = 0; s < (PAIR ? 0 : 2); ++s) sw[s] = exact_symbol<SF, MODE>(a, x, q, s, row, l, tid, red);
+    if constexpr (!PAIR) {  // two straight-line calls: sw[] stays in registers
+      sw[0] = exact_symbol<SF, MODE>(a, x, q, 0, row, l, tid, red);
+      sw[1] = exact_symbol<SF, MODE>(a, x, q, 1, row, l, tid, red);
+    }
     if (l == 0 && valid) {
       const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
       const uint8_t word = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
