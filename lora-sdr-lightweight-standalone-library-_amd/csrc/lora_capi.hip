@@ -140,7 +140,7 @@ int frame_max_blocks(int64_t frame_len) {
 // uses the first slot), the exact FrameParams, the pre-pass FrameParams and one
 // (margin, window max) pair per data symbol.
 struct WsLayout {
-  size_t fp, fp_spec, marg, total;
+  size_t fp, fp_spec, marg, fix, total;
 };
 WsLayout ws_layout(int64_t frames, int64_t frame_len, int step) {
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -149,7 +149,9 @@ WsLayout ws_layout(int64_t frames, int64_t frame_len, int step) {
   w.fp = al((size_t)frames * frame_max_blocks(frame_len) * sizeof(uint32_t));
   w.fp_spec = w.fp + al((size_t)frames * sizeof(lora::FrameParams));
   w.marg = w.fp_spec + al((size_t)frames * sizeof(lora::FrameParams));
-  w.total = w.marg + al((size_t)frames * per * 2 * sizeof(float));
+  w.fix = w.marg + al((size_t)frames * per * 2 * sizeof(float));
+  // the certification's reject list: a count, then up to every data symbol's (frame, j)
+  w.total = w.fix + al(256 + (size_t)frames * per * 2 * sizeof(uint32_t));
   return w;
 }
 
@@ -969,6 +971,8 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.spec_marg = reinterpret_cast<float*>(wsb + wl.marg);
   a.spec_max = maxbits;
   a.spec_fix = plan->spec_fix;
+  a.fix_count = reinterpret_cast<unsigned int*>(wsb + wl.fix);
+  a.fix_list = reinterpret_cast<uint32_t*>(wsb + wl.fix + 256);
   a.syms = out->symbols;
   a.sym_stride = out->sym_stride;
   a.sync = out->sync;
@@ -1031,6 +1035,10 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     if (ok) {
       ProfScope ps(plan, 1, st);
       ok = lora::launch_spec(as, frames, 2, st);
+    }
+    if (ok) {
+      ProfScope ps(plan, 1, st);
+      ok = lora::launch_spec(as, frames, 3, st);
     }
     if (!ok) rc = set_error(LORA_EIO, "speculative pipeline launch failed");
     kernels |= LORA_KERNEL_SPEC | LORA_KERNEL_ESTIMATE | LORA_KERNEL_DEMOD;

@@ -1148,12 +1148,10 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint64_t red[4];
   __shared__ FrameParams sp[SPB];
-  // SPEC == 2: per frame group, one bit per data symbol that failed certification
-  // (frames of up to kSpecChunks * T data symbols)
-  __shared__ unsigned long long fmask[SPEC == 2 ? SPB : 1][SPEC == 2 ? T : 1];
   const int tid = threadIdx.x;
   LORA_ESTAMP(5, true);
   LORA_ESTAMP(0, false);
+  if (SPEC == 1 && blockIdx.x == 0 && tid == 0) *a.fix_count = 0;  // the certification's reject list
   const int step = DYN ? a.step : N;
   const int osr = DYN ? a.osr : 1;
   const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
@@ -1469,15 +1467,13 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     // With n1 = 2 N max(|re|, |im|) over the window >= sum_i |y_i|, each bin moves by less
     // than B = n1 (|r - r'| L + e_ref + e_spec + 2 E) between the paths, so a speculative
     // top bin ahead of the runner-up by d > 2 B is the reference's argmax, strictly (no
-    // tie to break).  The kernel requires d > 4 B; a symbol that fails is recomputed
-    // exactly below with the reference's arithmetic (lora_demod_spec_recomputed() counts
-    // them).
+    // tie to break).  The kernel requires d > 4 B; a symbol that fails is listed and
+    // recomputed exactly with the reference's arithmetic by k_spec_fix, the pipeline's
+    // fourth launch, across the whole GPU (lora_demod_spec_recomputed() counts them).
     const FrameParams qs = a.fp_spec[f];
     const int per = a.total - 2;
     const bool same_t = qs.t_off == q.t_off;
-    for (int w = l; w < T; w += T) fmask[g][w] = 0;
-    block_sync<G::WAVE_LOCAL>();
-    {
+    if (valid) {
       const double u = 1.0 / 16777216.0;
       const double E = (8.0 * SF + 32.0) * u;
       const double drate = fabs((double)q.rate - (double)qs.rate);
@@ -1492,24 +1488,45 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
         const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
         const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
-        if (!(same_t && (double)v.x > 4.0 * B)) atomicOr(&fmask[g][j >> 6], 1ull << (j & 63));
-      }
-    }
-    block_sync<G::WAVE_LOCAL>();
-    LORA_ESTAMP(7, false);
-    for (int w = 0; w < (per + 63) >> 6; ++w) {  // group-uniform: every lane reads the same words
-      unsigned long long m = fmask[g][w];
-      while (m) {
-        const int j = w * 64 + __builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t idx = exact_symbol<SF, MODE>(a, x, q, 2 + j, row, l, tid, red);
-        if (l == 0 && valid) {
-          if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)idx;
-          atomicAdd(a.spec_fix, 1u);
+        if (!(same_t && (double)v.x > 4.0 * B)) {  // rejected: listed for k_spec_fix
+          const unsigned k = atomicAdd(a.fix_count, 1u);
+          a.fix_list[2 * (size_t)k] = (uint32_t)f;
+          a.fix_list[2 * (size_t)k + 1] = (uint32_t)j;
         }
       }
     }
+    LORA_ESTAMP(7, false);
     LORA_ESTAMP(6, true);
+  }
+}
+
+// k_spec_fix: the pipeline's fourth launch.  Every data symbol the certification
+// rejected (k_est_fast<SPEC = 2>'s list: frame, data symbol) recomputed exactly with the
+// frame's exact offsets a.fp[f] (LoRaDemod.cpp:137-175), one T-lane group per symbol, the
+// list spread over the whole grid - a frame with many rejected symbols no longer holds its
+// certify workgroup while the others idle.  gstride = grid * SPW list entries per round.
+template <int SF, int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+LORA_SCALAR_FP32 k_spec_fix(KArgs a, int rowc, int64_t gstride) {
+  using G = Geo<SF>;
+  constexpr int T = G::T, SPW = G::SPW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint64_t red[4];
+  const int tid = threadIdx.x;
+  const int g = SPW == 1 ? 0 : tid / T;
+  const int l = tid % T;
+  const int64_t count = (int64_t)__builtin_nontemporal_load(a.fix_count);
+  if (blockIdx.x == 0 && tid == 0 && count > 0) atomicAdd(a.spec_fix, (unsigned)count);
+  cf* row = reinterpret_cast<cf*>(smem) + (size_t)g * rowc;
+  for (int64_t i0 = (int64_t)blockIdx.x * SPW; i0 < count; i0 += gstride) {  // workgroup-uniform
+    const int64_t i = i0 + g;
+    const bool valid = i < count;
+    const int64_t k = valid ? i : count - 1;  // spare slots mirror the last entry
+    const int64_t f = a.fix_list[2 * k];
+    const int j = (int)a.fix_list[2 * k + 1];
+    const FrameParams q = a.fp[f];
+    const uint32_t idx = exact_symbol<SF, MODE>(a, a.iq + f * a.frame_stride, q, 2 + j, row, l, tid, red);
+    if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)idx;
   }
 }
 
@@ -1547,6 +1564,7 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
   const int tid = threadIdx.x;
   LORA_ESTAMP(5, true);
   LORA_ESTAMP(0, false);
+  if (blockIdx.x == 0 && tid == 0) *a.fix_count = 0;  // the certification's reject list
   const int g2 = tid / T;     // lane group: frame slot fg, symbol sym
   const int fg = g2 >> 1;
   const int sym = g2 & 1;
@@ -1770,7 +1788,26 @@ bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
   return true;
 }
 
-// The speculative pipeline's three launches for SF 6-12, MODE 0/1 (see lora_capi.hip).
+// k_spec_fix's grid: two workgroups per CU (or fewer when the frames hold fewer data
+// symbols); it reads the list's length on the device, so the launch does not wait for it.
+template <int SF, int MODE>
+bool launch_spec_fix(const KArgs& a, int64_t frames, hipStream_t st) {
+  using G = Geo<SF>;
+  const int rowc = row_complex<SF>();
+  const size_t lds = sizeof(cf) * (size_t)G::SPW * rowc;
+  if (lds > 160 * 1024) return false;
+  if (lds > 64 * 1024)
+    if (hipFuncSetAttribute((const void*)k_spec_fix<SF, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return false;
+  const int64_t most = (frames * (int64_t)(a.total - 2) + G::SPW - 1) / G::SPW;
+  const int64_t cap = (int64_t)device_cus() * 2;
+  const int64_t grid = std::max<int64_t>(1, std::min(most, cap));
+  launch(k_spec_fix<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, rowc, grid * G::SPW);
+  return true;
+}
+
+// The speculative pipeline's four launches for SF 6-12, MODE 0/1 (see lora_capi.hip).
 template <int SF>
 bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   if constexpr (SF < 6) {
@@ -1779,6 +1816,7 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
     if constexpr (SF <= 9 && LORA_EST_SPLIT) {
       if (stage == 0) return a.dechirp ? launch_est_split<SF, 0>(a, frames, st) : launch_est_split<SF, 1>(a, frames, st);
     }
+    if (stage == 3) return a.dechirp ? launch_spec_fix<SF, 0>(a, frames, st) : launch_spec_fix<SF, 1>(a, frames, st);
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
     if (stage == 1)
       return a.dechirp ? launch_spec_demod<SF, 0>(a, frames, st) : launch_spec_demod<SF, 1>(a, frames, st);

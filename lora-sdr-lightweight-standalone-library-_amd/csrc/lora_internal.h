@@ -50,6 +50,10 @@ struct KArgs {
   float* spec_marg = nullptr;      // [frame][data symbol][2]: |X1| - |X2|, window max(|I|,|Q|)
   uint32_t* spec_max = nullptr;    // writable alias of maxbits: [frame] max outside the windows
   unsigned int* spec_fix = nullptr;
+  // the symbols certification rejected, compacted: a count (zeroed by the pre-pass) and
+  // (frame, data symbol) pairs, recomputed exactly by the pipeline's fourth launch
+  unsigned int* fix_count = nullptr;
+  uint32_t* fix_list = nullptr;
 };
 
 // Shape of the fast kernels' LDS passes for SF >= 6 (lora_demod_fast.hip Geo<SF>): pass-1
@@ -92,10 +96,11 @@ void host_gen_chirp(std::complex<float>* out, int N, int osr, int NN, float f0, 
 bool launch_demod_fast(const KArgs& a, int s0, int64_t work, hipStream_t st);
 
 // Speculative single-read pipeline, SF 6-12, LEGACY osr-1 unwindowed frames with >= 3
-// symbols (lora_capi.hip): stage 0 = k_est_fast<SPEC=1> (estimate on unscaled samples +
-// the maximum outside the data windows), 1 = k_demod_fast<SPEC> (every data symbol, window
-// maxima and certification margins), 2 = k_est_fast<SPEC=2> (exact estimate, outputs,
-// sync word, certification and exact recomputation).  a.mx_bpf = 1.
+// symbols (lora_capi.hip): stage 0 = the pre-pass (estimate on unscaled samples + the
+// maximum outside the data windows), 1 = k_spec_demod (every data symbol, window maxima
+// and certification margins), 2 = k_est_fast<SPEC=2> (exact estimate, outputs, sync word,
+// certification; rejected symbols listed), 3 = k_spec_fix (the listed symbols recomputed
+// exactly).  a.mx_bpf = 1.
 bool launch_spec(const KArgs& a, int64_t frames, int stage, hipStream_t st);
 
 // Offset estimate + sync symbols with the same FFT machinery, one lane group per frame
