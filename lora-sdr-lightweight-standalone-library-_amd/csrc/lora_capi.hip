@@ -648,6 +648,7 @@ struct lora_demod_plan {
   std::vector<hipEvent_t> prof_pool;
   std::vector<ProfRec> prof_recs;
   int prof_max = 0, prof_calls = 0;
+  bool prof_short = false;  // the event pool ran out: the stage sums would be short
 };
 
 namespace {
@@ -661,6 +662,7 @@ struct ProfScope {
   hipEvent_t e = nullptr;
   ProfScope(lora_demod_plan* p, int s, hipStream_t stream) : plan(p), st(stream), stage(s) {
     on = plan->prof_calls < plan->prof_max && plan->prof_pool.size() >= 2;
+    if (plan->prof_calls < plan->prof_max && !on) plan->prof_short = true;  // a launch went untimed
     if (on) {
       hipEvent_t b = plan->prof_pool.back();
       plan->prof_pool.pop_back();
@@ -853,10 +855,11 @@ int lora_demod_profile_enable(lora_demod_plan* plan, int max_calls) {
   }
   for (hipEvent_t e : plan->prof_pool) hipEventDestroy(e);
   plan->prof_recs.clear();
-  plan->prof_pool.assign((size_t)max_calls * 3 * 2, nullptr);
+  plan->prof_pool.assign((size_t)max_calls * 4 * 2, nullptr);  // up to four launches per call
   for (auto& e : plan->prof_pool) HIP_TRY(hipEventCreate(&e));
   plan->prof_max = max_calls;
   plan->prof_calls = 0;
+  plan->prof_short = false;
   HIP_TRY(hipSetDevice(prev));
   return LORA_OK;
 }
@@ -865,6 +868,7 @@ int lora_demod_profile_read(lora_demod_plan* plan, float* stage_ms, int* calls) 
   if (!plan || !stage_ms || !calls) return set_error(LORA_EINVAL, "bad argument");
   for (int k = 0; k < 3; ++k) stage_ms[k] = 0.0f;
   *calls = plan->prof_calls;
+  if (plan->prof_short) return set_error(LORA_ERANGE, "profile event pool exhausted: stage times incomplete");
   for (auto& r : plan->prof_recs) {
     HIP_TRY(hipEventSynchronize(r.e));
     float ms = 0.0f;

@@ -21,9 +21,15 @@ __global__ void __launch_bounds__(256) k(float* out, float s) {
     } else if (MODE == 3) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(d[i]) : "v"((double)s));
-    } else {
+    } else if (MODE == 4) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) asm volatile("v_pk_mul_f32 %0, %0, %1 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "+v"(b[i]) : "v"(f2v{s, s}));
+    } else if (MODE == 5) {  // packed FMA, 8 independent chains
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(b[i]) : "v"(f2v{s, s}));
+    } else {  // scalar FMA, 16 independent chains
+#pragma unroll
+      for (int i = 0; i < 16; ++i) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(a[i]) : "v"(s));
     }
   }
   float r = 0;
@@ -47,5 +53,6 @@ float run(float* out, int blocks, int ninst) {
 int main() {
   float* out; hipMalloc(&out, 4096 * 256 * 4);
   run<0>(out, 4096, 16); run<1>(out, 4096, 8); run<2>(out, 4096, 8); run<3>(out, 4096, 8); run<4>(out, 4096, 8);
+  run<5>(out, 4096, 8); run<6>(out, 4096, 16);
   return 0;
 }
