@@ -1195,7 +1195,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         if (a.cfo) a.cfo[f] = qs.cfo;
         if (a.toff) a.toff[f] = qs.toff;
         if (a.max_amp) a.max_amp[f] = maxv;
-        if (a.sync) a.sync[f] = (uint8_t)qs.pad0;
       }
     }
   }
@@ -1390,15 +1389,17 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       const uint64_t mk = symbol_key<SF>((uint64_t)__float_as_uint(m) << 32, tid, red);
       (void)per;
       if (l == 0 && valid) a.spec_max[f] = (uint32_t)(mk >> 32);
-      // Already above 1: the frame is rescaled, so k_est_fast<SPEC = 2> recomputes the
-      // estimate and the sync word; skip them here (frame-uniform exit).
-      if (__uint_as_float((uint32_t)(mk >> 32)) > 1.0f) {
-        LORA_ESTAMP(4, false);
-        LORA_ESTAMP(6, true);
-        return;
-      }
-      block_sync<G::WAVE_LOCAL>();  // red is reused by the sync symbols
+      // The sync word waits for the exact offsets: k_est_fast<SPEC = 2> computes it.
+      LORA_ESTAMP(4, false);
+      LORA_ESTAMP(6, true);
+      return;
     }
+  }  // exact estimate
+  // The sync symbols with the frame's offsets (LoRaDemod.cpp:137-168, 177-192; phy.cpp:
+  // 228-237); in the speculative pipeline only in stage 2, once the exact offsets are known.
+  if constexpr (SPEC != 1) {
+    constexpr bool PAIR = EstGeo<SF>::PAIR && MODE <= 1;
+    cf in[P], z[P];
     uint32_t sw[2];
     if constexpr (PAIR) {
       cf* row1 = row + (size_t)EstGeo<SF>::SPB * rowc;
@@ -1423,21 +1424,12 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       sw[0] = exact_symbol<SF, MODE>(a, x, q, 0, row, l, tid, red);
       sw[1] = exact_symbol<SF, MODE>(a, x, q, 1, row, l, tid, red);
     }
-    if (l == 0 && valid) {
+    if (l == 0 && valid && a.sync) {
       const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
-      const uint8_t word = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
-      if constexpr (SPEC == 1) {
-        a.fp_spec[f].pad0 = word;  // the pre-pass sync word, final when the frame is not rescaled
-      } else if (a.sync) {
-        a.sync[f] = word;
-      }
+      a.sync[f] = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
     }
     LORA_ESTAMP(4, false);
-    if constexpr (SPEC == 1) {
-      LORA_ESTAMP(6, true);
-      return;
-    }
-  }  // exact estimate
+  }
   if constexpr (SPEC == 2) {
     // ---- certification of the data symbols the demod computed speculatively ----
     // The demod used the pre-pass offsets qs (rate r', t_off) on the unscaled samples y;
@@ -1504,10 +1496,11 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
 // rejected (k_est_fast<SPEC = 2>'s list: frame, data symbol) recomputed exactly with the
 // frame's exact offsets a.fp[f] (LoRaDemod.cpp:137-175), one T-lane group per symbol, the
 // list spread over the whole grid - a frame with many rejected symbols no longer holds its
-// certify workgroup while the others idle.  gstride = grid * SPW list entries per round.
+// certify workgroup while the others idle.  Entry i goes to workgroup i % grid, so a short
+// list still spreads over every CU (slot g of round r: i = blockIdx.x + grid (r SPW + g)).
 template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-LORA_SCALAR_FP32 k_spec_fix(KArgs a, int rowc, int64_t gstride) {
+LORA_SCALAR_FP32 k_spec_fix(KArgs a, int rowc, int64_t grid) {
   using G = Geo<SF>;
   constexpr int T = G::T, SPW = G::SPW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1518,8 +1511,8 @@ LORA_SCALAR_FP32 k_spec_fix(KArgs a, int rowc, int64_t gstride) {
   const int64_t count = (int64_t)__builtin_nontemporal_load(a.fix_count);
   if (blockIdx.x == 0 && tid == 0 && count > 0) atomicAdd(a.spec_fix, (unsigned)count);
   cf* row = reinterpret_cast<cf*>(smem) + (size_t)g * rowc;
-  for (int64_t i0 = (int64_t)blockIdx.x * SPW; i0 < count; i0 += gstride) {  // workgroup-uniform
-    const int64_t i = i0 + g;
+  for (int64_t r0 = 0; (int64_t)blockIdx.x + grid * r0 < count; r0 += SPW) {  // workgroup-uniform
+    const int64_t i = (int64_t)blockIdx.x + grid * (r0 + g);
     const bool valid = i < count;
     const int64_t k = valid ? i : count - 1;  // spare slots mirror the last entry
     const int64_t f = a.fix_list[2 * k];
@@ -1560,7 +1553,6 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ FrameParams sp[FPW];
   __shared__ float tail[FPW][2][4];  // per frame and symbol: index, fractional index, phase, -
-  __shared__ uint32_t sws[FPW][2];
   const int tid = threadIdx.x;
   LORA_ESTAMP(5, true);
   LORA_ESTAMP(0, false);
@@ -1664,31 +1656,7 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
       }
       m = frame_max(m);
       if (l2 == 0 && valid) a.spec_max[f] = __float_as_uint(m);
-      // already above 1: rescaled, stage 2 recomputes the estimate and the sync word
-      if (m > 1.0f) {  // frame-uniform
-        LORA_ESTAMP(4, false);
-        LORA_ESTAMP(6, true);
-        return;
-      }
-    }
-    // the sync symbols with the estimated offsets (LoRaDemod.cpp:137-168, 177-192),
-    // symbol `sym` on this group
-    {
-      int64_t base;
-      int cg;
-      sym_base(sym, N, a.frame_len, q.t_off, base, cg);
-      const float start = q.rate * ((float)((uint32_t)sym * (uint32_t)N) + (float)q.t_off);
-      gather_points<SF>(a, x + base, l, 1, N, cg, 1, dech, q.scaled ? q.scale : 1.0f, in);
-      rotate_place<SF, true>(in, z, start, q.rate, false, a.win, l);
-      uint64_t k2 = fft_key<SF, false>(z, row, l, a);
-      k2 = group_max(k2, T);
-      if (l == 0) sws[fg][sym] = key_index(k2);
-      wave_sync();
-    }
-    if (l2 == 0 && valid) {
-      const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
-      const uint8_t word = (uint8_t)((((sws[fg][0] >> shift) & 0x0f) << 4) | ((sws[fg][1] >> shift) & 0x0f));
-      a.fp_spec[f].pad0 = word;  // the pre-pass sync word, final when the frame is not rescaled
+      // the sync word waits for the exact offsets (k_est_fast<SPEC = 2>)
     }
     LORA_ESTAMP(4, false);
     LORA_ESTAMP(6, true);
@@ -1803,7 +1771,7 @@ bool launch_spec_fix(const KArgs& a, int64_t frames, hipStream_t st) {
   const int64_t most = (frames * (int64_t)(a.total - 2) + G::SPW - 1) / G::SPW;
   const int64_t cap = (int64_t)device_cus() * 2;
   const int64_t grid = std::max<int64_t>(1, std::min(most, cap));
-  launch(k_spec_fix<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, rowc, grid * G::SPW);
+  launch(k_spec_fix<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, rowc, grid);
   return true;
 }
 
