@@ -1480,10 +1480,21 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
         const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
         const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
-        if (!(same_t && (double)v.x > 4.0 * B)) {  // rejected: listed for k_spec_fix
-          const unsigned k = atomicAdd(a.fix_count, 1u);
-          a.fix_list[2 * (size_t)k] = (uint32_t)f;
-          a.fix_list[2 * (size_t)k + 1] = (uint32_t)j;
+        // rejected: listed for k_spec_fix, one list reservation per wave (a -10 dB batch
+        // rejects thousands of symbols: per-lane atomics on one counter serialise)
+        const bool rej = !(same_t && (double)v.x > 4.0 * B);
+        const uint64_t m = __ballot(rej);
+        if (m) {
+          const int lane = (int)__lane_id();
+          const int first = __builtin_ctzll(m);
+          unsigned base = 0;
+          if (lane == first) base = atomicAdd(a.fix_count, (unsigned)__popcll(m));
+          base = (unsigned)__shfl((int)base, first, 64);
+          if (rej) {
+            const size_t k = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
+            a.fix_list[2 * k] = (uint32_t)f;
+            a.fix_list[2 * k + 1] = (uint32_t)j;
+          }
         }
       }
     }

@@ -33,7 +33,7 @@ def stats(d):
 def main():
     src = sys.argv[1]
     out = []
-    for tag in ("kt7", "kt12"):
+    for tag in ("kt7", "kt7n10", "kt12"):
         rows = stats(os.path.join(src, tag))
         if not rows:
             continue
@@ -49,7 +49,7 @@ def main():
                 continue
             out.append(f"| `{k}` | {wg} | {a['n']} | {a['ns'] / a['n'] / 1e3:.2f} | {a['lds']} | {a['vgpr']} | {a['scratch']} |")
         # step structure: consecutive pipeline kernels; gaps between a kernel's end and the next start
-        pipe = [r for r in rows if r[0].startswith(("k_est_fast", "k_est_split", "k_spec_demod", "k_demod_fast", "k_frame_max"))]
+        pipe = [r for r in rows if r[0].startswith(("k_est_fast", "k_est_split", "k_spec_fix", "k_spec_demod", "k_demod_fast", "k_frame_max"))]
         gaps = [pipe[i + 1][1] - pipe[i][2] for i in range(len(pipe) - 1)]
         if gaps:
             gaps.sort()

@@ -1,0 +1,27 @@
+#!/usr/bin/env python3
+"""One bench workload alone, for a profiler: the pipeline over `frames` frames of 2 + 64
+symbols (bench.py's make_input: GPU modulation, optional AWGN at `snr` dB), `steps`
+times.  usage: prof_workload.py <sf> [snr_db|none] [frames] [steps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "lora-sdr-lightweight-standalone-library-_amd"))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import lora_phy_amd as amd  # noqa: E402
+
+sf = int(sys.argv[1])
+snr = None if len(sys.argv) < 3 or sys.argv[2] == "none" else float(sys.argv[2])
+frames = int(sys.argv[3]) if len(sys.argv) > 3 else 15625
+steps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+dev = torch.device("cuda", 0)
+_, iq = bench.make_input(sf, frames, 64, 20251015, dev, snr)
+plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=dev)
+out = None
+for _ in range(steps):
+    out = plan.run(iq, out)
+torch.cuda.synchronize()
+print("recomputed", plan.spec_recomputed(), "kernels", plan.last_kernels())
