@@ -1472,17 +1472,23 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
       const double tabs = (double)abs(q.t_off);
       const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
+      // the certification tests (eight margin loads in flight per lane), then the rejected
+      // symbols listed for k_spec_fix: one list reservation per wave and round (a -10 dB
+      // batch rejects thousands of symbols; per-lane atomics on one counter serialise)
+      uint64_t rejbits = 0;  // bit k: symbol l + T k (per <= kSpecChunks T)
 #pragma unroll 8
-      for (int j = l; j < per; j += T) {
+      for (int j = l, k = 0; j < per; j += T, ++k) {
         const float2 v = mg[j];
         const double n1 = 2.0 * N * (double)v.y;
         const double L = (double)(3 + j) * N + tabs;
         const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
         const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
         const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
-        // rejected: listed for k_spec_fix, one list reservation per wave (a -10 dB batch
-        // rejects thousands of symbols: per-lane atomics on one counter serialise)
-        const bool rej = !(same_t && (double)v.x > 4.0 * B);
+        if (!(same_t && (double)v.x > 4.0 * B)) rejbits |= 1ull << k;
+      }
+      const int rounds = (per + T - 1) / T;  // uniform
+      for (int k = 0; k < rounds; ++k) {
+        const bool rej = (rejbits >> k) & 1;
         const uint64_t m = __ballot(rej);
         if (m) {
           const int lane = (int)__lane_id();
@@ -1491,9 +1497,9 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
           if (lane == first) base = atomicAdd(a.fix_count, (unsigned)__popcll(m));
           base = (unsigned)__shfl((int)base, first, 64);
           if (rej) {
-            const size_t k = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
-            a.fix_list[2 * k] = (uint32_t)f;
-            a.fix_list[2 * k + 1] = (uint32_t)j;
+            const size_t slot = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
+            a.fix_list[2 * slot] = (uint32_t)f;
+            a.fix_list[2 * slot + 1] = (uint32_t)(l + T * k);
           }
         }
       }
