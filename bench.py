@@ -258,7 +258,10 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
         "msym_s_data": frames * data_syms / (ms_step * 1e-3) / 1e6,
         "msym_s_all_ranks": units / wall_max / 1e6, "ms_per_step_max_rank": wall_max * 1e3 / steps,
         "msym_s_all": frames * total_syms / (ms_step * 1e-3) / 1e6,
-        "dominant_kernel": ["k_frame_max", "k_est_fast", "k_demod_fast"][dom], "dominant_stage": dom,
+        # stage 2 is the symbol pass: k_spec_demod in the speculative pipeline (the default),
+        # k_demod_fast in the three-launch one
+        "dominant_kernel": ["k_frame_max", "k_est_fast",
+                            "k_spec_demod" if "spec" in kernels else "k_demod_fast"][dom], "dominant_stage": dom,
         "dominant_gbs": dom_gbs, "dominant_bytes_per_launch": dom_bytes,
         "step_bytes": step_bytes, "pipeline_gbs": step_bytes / (ms_step * 1e-3) / 1e9,
         "plan": plan, "iq": iq, "syms": syms, "out": out,
@@ -484,8 +487,8 @@ def roofline(r, probe=None):
             "frac": r["dominant_gbs"] / HBM_PEAK_GBS,
             "bytes_per_launch": r["dominant_bytes_per_launch"],
             "traffic": pmc_dom,
-            "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, committed; "
-                              "not measured in this run)",
+            "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch, "
+                              "tools/pmc_r03.py; committed, not measured in this run)",
             "pipeline": {"algorithmic_bytes_per_step": r["step_bytes"], "ms_per_step": r["ms_per_step"],
                          "achieved": r["pipeline_gbs"], "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS,
                          "counter_bytes_per_step": pmc_step,

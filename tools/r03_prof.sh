@@ -22,4 +22,13 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
     timeout -s KILL 150 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- python3 tools/prof_workload.py $cfg > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -3 $OUT/pmc$i.log; exit 2; }
   done
 done
+# HBM traffic: FETCH_SIZE and WRITE_SIZE in passes of their own (TCC slots), per workload
+for cfg in "7 none 15625 2" "12 none 4000 2"; do
+  sf=${cfg%% *}
+  for c in FETCH_SIZE WRITE_SIZE; do
+    tag=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
+    echo "== $c sf$sf $(date +%T)"
+    timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$tag$sf -o run -- python3 tools/prof_workload.py $cfg > $OUT/pmc_$tag$sf.log 2>&1 || { echo "$c pass failed"; tail -3 $OUT/pmc_$tag$sf.log; exit 2; }
+  done
+done
 echo "== done $(date +%T)"
