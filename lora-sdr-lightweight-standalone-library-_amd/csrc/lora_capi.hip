@@ -137,21 +137,28 @@ int frame_max_blocks(int64_t frame_len) {
 
 // Workspace of one lora_demod_batch call, sized from the frames (no zeroing pass, no
 // atomics on it): per-frame partial maxima (k_frame_max blocks; the speculative pipeline
-// uses the first slot), the exact FrameParams, the pre-pass FrameParams and one
-// (margin, window max) pair per data symbol.
+// uses the first slot), the exact FrameParams, the pre-pass FrameParams, one 8-byte
+// speculative entry per symbol and the certification's reject list.
 struct WsLayout {
   size_t fp, fp_spec, marg, fix, total;
+  int64_t fix_cap;  // entries per stripe of the reject list
 };
-WsLayout ws_layout(int64_t frames, int64_t frame_len, int step) {
+WsLayout ws_layout(int64_t frames, int64_t frame_len, int step, int N) {
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-  const int64_t per = std::max<int64_t>(0, frame_len / step - 2);
+  const int64_t total = std::max<int64_t>(0, frame_len / step);
+  const int64_t per = std::max<int64_t>(0, total - 2);
   WsLayout w;
   w.fp = al((size_t)frames * frame_max_blocks(frame_len) * sizeof(uint32_t));
   w.fp_spec = w.fp + al((size_t)frames * sizeof(lora::FrameParams));
   w.marg = w.fp_spec + al((size_t)frames * sizeof(lora::FrameParams));
-  w.fix = w.marg + al((size_t)frames * per * 2 * sizeof(float));
-  // the certification's reject list: a count, then up to every data symbol's (frame, j)
-  w.total = w.fix + al(256 + (size_t)frames * per * 2 * sizeof(uint32_t));
+  // one 8-byte entry per symbol (KArgs::spec_marg)
+  w.fix = w.marg + al((size_t)frames * total * 2 * sizeof(float));
+  // the certification's reject list: kFixStripes counts, then per stripe up to every data
+  // symbol's (frame, j) and one sync-word entry per frame of its workgroups
+  const int64_t spb = lora::est_frames_per_block(N);
+  const int64_t wgs = (frames + spb - 1) / spb;
+  w.fix_cap = (wgs + lora::kFixStripes - 1) / lora::kFixStripes * spb * (per + 1);
+  w.total = w.fix + al(64 * lora::kFixStripes + (size_t)lora::kFixStripes * w.fix_cap * 2 * sizeof(uint32_t));
   return w;
 }
 
@@ -909,7 +916,7 @@ int64_t lora_demod_symbols_per_frame(const lora_demod_plan* plan, int64_t frame_
 
 size_t lora_demod_workspace_bytes(const lora_demod_plan* plan, int64_t frames, int64_t frame_len) {
   if (!plan || frames <= 0 || frame_len < 0) return 0;
-  return ws_layout(frames, frame_len, plan->step).total;
+  return ws_layout(frames, frame_len, plan->step, plan->N).total;
 }
 
 int64_t lora_demod_spec_recomputed(lora_demod_plan* plan) {
@@ -932,7 +939,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   if (!iq) return set_error(LORA_EINVAL, "null iq");
   if (out->symbols && out->sym_stride < nsym)
     return set_error(LORA_ERANGE, "sym_stride smaller than symbols per frame");  // phy.cpp:190
-  const WsLayout wl = ws_layout(frames, frame_len, plan->step);
+  const WsLayout wl = ws_layout(frames, frame_len, plan->step, plan->N);
   const size_t need = wl.total;
   if (!workspace || workspace_bytes < need)
     return set_error(LORA_ERANGE, "workspace too small");
@@ -976,7 +983,8 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   a.spec_max = maxbits;
   a.spec_fix = plan->spec_fix;
   a.fix_count = reinterpret_cast<unsigned int*>(wsb + wl.fix);
-  a.fix_list = reinterpret_cast<uint32_t*>(wsb + wl.fix + 256);
+  a.fix_list = reinterpret_cast<uint32_t*>(wsb + wl.fix + 64 * lora::kFixStripes);
+  a.fix_cap = wl.fix_cap;
   a.syms = out->symbols;
   a.sym_stride = out->sym_stride;
   a.sync = out->sync;
@@ -1011,19 +1019,23 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     if (e != hipSuccess) rc = set_error(LORA_EIO, "hipMemsetAsync failed");
   }
   // Speculative single-read pipeline (LoRaDemod.cpp:59-192 reordered, results identical):
-  //   1. offset estimate on UNSCALED samples (k_est_fast<SPEC=1>), plus the maximum of the
-  //      samples outside the data-symbol windows it implies;
-  //   2. every data symbol with those offsets on unscaled samples (k_demod_fast<SPEC>),
-  //      which also reduces each window's max(|I|,|Q|) - the frame-max pass's work, from
-  //      the same read - and records the symbol's argmax margin;
-  //   3. the exact estimate from the assembled maximum (k_est_fast<SPEC=2>): outputs, sync
-  //      word, and each speculative symbol either certified (its margin exceeds the
-  //      rounding bound, so the reference's argmax is the same bin) or recomputed exactly.
+  //   1. offset estimate on UNSCALED samples (k_est_split / k_est_fast<SPEC=1>), plus the
+  //      maximum of the samples outside the data-symbol windows it implies;
+  //   2. every symbol with those offsets on unscaled samples (k_spec_demod), which also
+  //      reduces each data window's max(|I|,|Q|) - the frame-max pass's work, from the same
+  //      read - and records each symbol's argmax margin;
+  //   3. the exact estimate from the assembled maximum (k_est_fast<SPEC=2>): outputs, and
+  //      each speculative symbol - sync symbols included - either certified (its margin
+  //      exceeds the rounding bound, so the reference's argmax is the same bin) or listed;
+  //   4. the listed symbols and sync words recomputed exactly (k_spec_fix).
   // The IQ is read once plus symbols 0/1 twice; lora_demod_spec_recomputed() counts
   // recomputations.  The symbol demod rotates with the hardware sine/cosine under either
-  // precision; the certification holds it to the EXACT reference.
+  // precision; the certification holds it to the EXACT reference.  A sync block of
+  // k_spec_demod spans 512/N frames (N < 1024): their byte offsets must fit 31 bits.
+  const int64_t sync_frames = plan->N < 1024 ? 512 / plan->N : 1;
   const bool spec_ok = plan->spec && p.mode == LORA_MODE_LEGACY && p.osr == 1 && !a.hann && p.sf >= 6 &&
-                       total >= 3 && total - 2 <= lora::kSpecChunks * (plan->N / 16);
+                       total >= 3 && total - 2 <= lora::kSpecChunks * (plan->N / 16) &&
+                       sync_frames * frame_stride * 8 < (int64_t(1) << 31);
   if (rc == LORA_OK && spec_ok) {
     KArgs as = a;
     as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows

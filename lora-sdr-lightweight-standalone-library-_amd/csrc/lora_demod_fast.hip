@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -885,31 +886,36 @@ __device__ __forceinline__ void stamp(int k, bool real) {
   if ((threadIdx.x & 63) == 0 && wv < (unsigned)kStampWaves) g_stamps[(size_t)wv * 8 + k] = t;
 }
 #define LORA_STAMP(k, real) \
-  if (r == 0) stamp(k, real)
+  if (first_round) stamp(k, real)
 #else
 #define LORA_STAMP(k, real)
 #define LORA_ESTAMP(k, real)
 #endif
 
 // ---- the speculative pipeline's symbol pass -----------------------------------------
-// k_spec_demod: every data symbol of LEGACY osr-1 unwindowed frames (MODE 0: fused caller
+// k_spec_demod: every symbol of LEGACY osr-1 unwindowed frames (MODE 0: fused caller
 // dechirp from the paired table KArgs::downP; MODE 1: dechirped input) with the pre-pass
-// offsets (fp_spec) on UNSCALED samples, the hardware rotation and fused multiply-adds,
-// the symbol's index, its top-bin / runner-up margin and its window's max(|I|,|Q|) (one
-// 8-byte spec_marg store), certified or recomputed exactly by k_est_fast<SPEC = 2>.  The
-// arithmetic is k_demod_fast<SF, MODE, true, true>'s.
-// Persistent: the work is cut into blocks of SPB consecutive data symbols of one frame
-// (a wave's 64/T symbols for T <= 64, the workgroup's SPW symbols beyond), so the frame,
-// its offsets and every address but the lane's own are wave-uniform (scalar registers
-// and scalar loads); a frame's last block may be partial.  A workgroup takes groups of BPG
-// blocks blockIdx.x, blockIdx.x + gstride, ... (gstride = the grid: a few workgroups per
-// CU, launch_spec_demod): short waves (about 4 us at SF7) left the CUs half occupied
-// between one workgroup's end and the next one's start.
+// offsets (fp_spec) on UNSCALED samples, the hardware rotation and fused multiply-adds:
+// per data symbol its index, top-bin / runner-up margin and window max(|I|,|Q|), per sync
+// symbol its margin and index (one 8-byte spec_marg entry each), all certified or
+// recomputed exactly by k_est_fast<SPEC = 2> / k_spec_fix.  The arithmetic is
+// k_demod_fast<SF, MODE, true, true>'s.
+// The work is cut into blocks of SPB symbols (a wave's 64/T for T <= 64, the workgroup's
+// SPW beyond): first every frame's data symbols, SPB consecutive ones of one frame per block
+// (a frame's last block may be partial), so the frame, its offsets and every address but
+// the lane's own are wave-uniform (scalar registers and loads); then the sync symbols, the
+// two of SPB/2 consecutive frames per block.  Persistent: a workgroup takes groups of BPG
+// blocks blockIdx.x, blockIdx.x + gstride, ... (gstride = the grid: a few workgroups per CU,
+// launch_spec_demod) - short waves (about 4 us at SF7) left the CUs half occupied between
+// one workgroup's end and the next one's start.
 #ifndef LORA_SPEC_PERSIST
 #define LORA_SPEC_PERSIST 1  // 1: wave-local geometries (SF <= 10), 2: every SF, 0: none
 #endif
-#ifndef LORA_SPEC_PREFETCH
-#define LORA_SPEC_PREFETCH 0
+#ifndef LORA_SPEC_ALIGN
+#define LORA_SPEC_ALIGN 1  // aligned gathers with lane roles (wave-local geometries)
+#endif
+#ifndef LORA_SPEC_SYNC_FIRST
+#define LORA_SPEC_SYNC_FIRST 0  // the sync blocks before the data blocks
 #endif
 template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
@@ -926,111 +932,108 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   __shared__ uint32_t red3[3 * 4];  // spec_reduce's cross-wave words (T > 64)
   cf* rows = reinterpret_cast<cf*>(smem);
   cf* twl = rows + (size_t)SPW * rowc;
-  const int per = a.total - 2;
+  const int tot = a.total;
+  const int per = tot - 2;
   if constexpr (NTW > 0) {
     const int tid = threadIdx.x;
     if (tid < NTW) twl[tid] = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
     __syncthreads();
   }
-  const int bpf = (per + SPB - 1) / SPB;  // blocks per frame
-  const int64_t blocks = frames * bpf;
+  const int bpf = (per + SPB - 1) / SPB;  // data blocks per frame
+  const int64_t dblocks = frames * bpf;
+  const int64_t blocks = dblocks + (2 * frames + SPB - 1) / SPB;
   const int64_t groups = (blocks + BPG - 1) / BPG;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   typedef float v2f __attribute__((ext_vector_type(2)));
-  // block b (wave-uniform) -> frame f, the lane's data symbol j and its window
-  struct Loc {
-    int64_t f, base;
-    int j, cg, toff;
-    float rate;
-    bool valid;
-  };
-  auto locate = [&](int64_t b, int g) {
-    Loc L;
-    L.f = b / bpf;
-    const int jl = (int)(b - L.f * bpf) * SPB + (WL ? (g % SPB) : g);
-    L.valid = jl < per;
-    L.j = L.valid ? jl : per - 1;  // a partial block's spare slots mirror a valid symbol
-    const FrameParams fp = a.fp_spec[L.f];
-    L.rate = fp.rate;
-    L.toff = fp.t_off;
-    sym_base(2 + L.j, N, a.frame_len, L.toff, L.base, L.cg);
-    return L;
-  };
-  // the window's samples (read once: nontemporal) through a buffer resource on the
-  // wave-uniform frame base: the point offsets T q (up to 30 KB at SF12) go in the scalar
-  // offset or the immediate, not in 64-bit vector adds.  Byte offsets fit 31 bits: the
-  // pipeline's frames hold < 2^26 samples.
-  auto load_iq = [&](const Loc& L, int l, cf* dst) {
-    const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + L.f * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
-    const int vo = (int)(L.base + l) * 8;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const v2f v = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
-      dst[q] = cf{v.x, v.y};
-    }
-  };
-  // PF: the next round's samples are requested during this round (its table values first:
-  // loads complete in order, so a table load issued after the prefetch would wait for it).
-  // Only where no vector load follows inside the transform (two-pass geometries, SF <= 8).
-  constexpr bool PF = LORA_SPEC_PREFETCH && G::NPASS == 2;
-  int64_t grp = blockIdx.x;
-  int64_t b = grp * BPG + (WL ? wave : 0);  // wave-uniform
-  bool have = grp < groups && (!WL || b < blocks);
-  cf nx[PF ? P : 1];
-  Loc nl{};
-  if constexpr (PF) {
-    if (have) {
-      const int tid = threadIdx.x;
-      nl = locate(b, SPW == 1 ? 0 : tid / T);
-      load_iq(nl, tid % T, nx);
-    }
-  }
-  for (int r = 0; have; ++r) {
-    (void)r;  // the round (diagnostic stamps of the first one)
+
+  // one block: SYNC = false a data block (frame-uniform), true a sync block
+  auto run_block = [&](auto sync_c, int64_t b, bool first_round) {
+    constexpr bool SYNC = decltype(sync_c)::value;
+    (void)first_round;  // the diagnostic stamps record a workgroup's first round
     // the lane index, opaque per round: left visible, the compiler hoists every lane
     // address out of the loop and keeps them live across it (more VGPRs, spills at SF12)
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     const int g = SPW == 1 ? 0 : tid / T;  // slot in the workgroup (its LDS row)
     const int l = tid % T;                 // lane within the symbol
+    const int gi = WL ? (g % SPB) : g;     // symbol within the block
     LORA_STAMP(5, true);
     LORA_STAMP(0, false);
-    const Loc L = PF ? nl : locate(b, g);
-    const int64_t f = L.f;
-    const int j = L.j, s = 2 + L.j, toff = L.toff;
-    const bool valid = L.valid;
-    const float rate = L.rate;
-    cf in[P];
-    if constexpr (PF) {
-#pragma unroll
-      for (int q = 0; q < P; ++q) in[q] = nx[q];
+    int64_t f, fu;  // the lane's frame; the block's first (wave-uniform)
+    int s;          // symbol within the frame
+    bool valid;
+    int rel = 0;    // byte offset of frame f from frame fu
+    if constexpr (!SYNC) {
+      if (LORA_SPEC_SYNC_FIRST) b -= blocks - dblocks;
+      f = fu = b / bpf;
+      const int jl = (int)(b - f * bpf) * SPB + gi;
+      valid = jl < per;
+      s = 2 + (valid ? jl : per - 1);  // a partial block's spare slots mirror a valid symbol
     } else {
-      load_iq(L, l, in);
+      const int64_t k0 = (LORA_SPEC_SYNC_FIRST ? b : b - dblocks) * SPB;
+      int64_t k = k0 + gi;
+      valid = k < 2 * frames;
+      if (!valid) k = 2 * frames - 1;
+      f = k >> 1;
+      s = (int)(k & 1);
+      fu = k0 >> 1;
+      rel = (int)((f - fu) * a.frame_stride * 8);  // < 2^31: lora_demod_batch checks the stride
     }
-    // the caller-side dechirp's table pairs (two values per 16-byte load)
+    const FrameParams fp = a.fp_spec[f];
+    const float rate = fp.rate;
+    const int toff = fp.t_off;
+    int64_t base;
+    int cg;
+    sym_base(s, N, a.frame_len, toff, base, cg);
+    // The window's samples (read once: nontemporal) through a buffer resource on the
+    // wave-uniform frame base: the point offsets T q (up to 30 KB at SF12) go in the scalar
+    // offset or the immediate, not in 64-bit vector adds.  Byte offsets fit 31 bits: the
+    // pipeline's frames hold < 2^26 samples.
+    // Alignment (wave-local geometries): a load instruction fetches T consecutive samples
+    // per symbol; a window at base = A + d (A a multiple of D = min(T, 8) samples, so the
+    // chunks never straddle a 128-byte line: one straddling in two cost the SF7 demod 19 %)
+    // is read from A instead, and lane l plays the role lr = (l - d) mod T of the FFT: its
+    // points lr + T q are the samples A + l + T q (l >= d) or A + l + T (q + 1) (l < d), so
+    // the lane takes 17 loads and selects.  The roles permute the lanes of each symbol, so
+    // the LDS accesses (and their banks) of every instruction are the same set.
+    constexpr int D = T < 8 ? T : 8;
+    constexpr bool AL = WL && LORA_SPEC_ALIGN;
+    const int d = AL ? (int)(base & (D - 1)) : 0;
+    const int lr = AL ? ((l - d) & (T - 1)) : l;
+    v2f ld[P + 1];
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + fu * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
+    const int vo = rel + (int)(base - d + l) * 8;
+    // with the caller-side dechirp's table pairs (two values per 16-byte load), issued in
+    // the order the products consume them (vmcnt retires in order: a table load issued
+    // after every sample would hold the first product until the last sample arrives -
+    // 7 % of the SF7 demod)
     float4 dt[MODE == 0 ? P / 2 : 1];
-    if constexpr (MODE == 0) {
-      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
-      const int vo = (L.cg + l) * 16;
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
+    const int vt = (cg + lr) * 16;
 #pragma unroll
-      for (int pp = 0; pp < P / 2; ++pp)
-        dt[pp] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vo, pp * (N + T) * 16, 0));
+    for (int pp = 0; pp < P / 2; ++pp) {
+      if constexpr (MODE == 0)
+        dt[pp] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vt, pp * (N + T) * 16, 0));
+#pragma unroll
+      for (int q = 2 * pp; q < 2 * pp + 2; ++q)
+        ld[q] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
     }
-    // the next round
-    grp += gstride;
-    b = grp * BPG + (WL ? wave : 0);
-    have = grp < groups && (!WL || b < blocks);
-    if constexpr (PF) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (have) {
-        nl = locate(b, g);
-        load_iq(nl, l, nx);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    if (AL && __builtin_amdgcn_readfirstlane(__ballot(d != 0) != 0)) {
+      // the 17th load: lanes l < d take window points; the others (whose load would fall up
+      // to T samples past the window, possibly past the batch) re-read load 15's sample
+      const bool late = l < d;
+      ld[P] = __builtin_bit_cast(
+          v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, late ? vo : vo - T * 8, P * T * 8, 2 /* nt */));
+#pragma unroll
+      for (int q = 0; q < P; ++q) ld[q] = late ? ld[q + 1] : ld[q];  // ascending: ld[q + 1] not yet moved
     }
+    cf in[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) in[q] = cf{ld[q].x, ld[q].y};
     // caller-side dechirp (e2e_chain_test.cpp:88-93) with the reference's products, the
-    // window's max(|I|,|Q|) of exactly these samples, then the rotation
+    // window's max(|I|,|Q|) of exactly these samples (data symbols: the pre-pass covered
+    // the sync windows), then the rotation
     if constexpr (MODE == 0) {
 #pragma unroll
       for (int pp = 0; pp < P / 2; ++pp) {
@@ -1039,36 +1042,49 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       }
     }
     float pm = 0.0f;
+    if constexpr (!SYNC) {
 #pragma unroll
-    for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
+      for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
+    }
     LORA_STAMP(1, false);
     const float start = rate * ((float)((uint32_t)s * (uint32_t)N) + (float)toff);
     cf z[P];
-    rotate_place<SF, true, true, true>(in, z, start, rate, false, a.win, l);
+    rotate_place<SF, true, true, true>(in, z, start, rate, false, a.win, lr);
     asm volatile("" : "+v"(pm));
     LORA_STAMP(2, false);
-    const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true>(z, rows + (size_t)g * rowc, l, a, nullptr, twl);
+    const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true>(z, rows + (size_t)g * rowc, lr, a, nullptr, twl);
     LORA_STAMP(3, false);
     // the symbol's best and runner-up keys over its lanes; the lane holding the best key
-    // stores the index (equal best keys in two lanes: a zero margin, so the certify kernel
-    // recomputes the symbol and overwrites it)
+    // has the index (equal best keys in two lanes: a zero margin, so the symbol is
+    // recomputed and overwritten)
     const uint32_t lbest = (uint32_t)lk;
     uint32_t best = lbest, sec = (uint32_t)(lk >> 32);
     spec_reduce<SF>(best, sec, pm, tid, red3);
     if (valid) {
       constexpr int NG = (G::NPASS == 2 ? P / G::RA : P / G::RB);
       constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
-      if (lbest == best && a.syms) {
-        const int o = (int)(best & 15u);  // ordinal u * NG + gg: bin = l + T gg + ML u
-        a.syms[f * a.sym_stride + j] = (uint16_t)(l + T * (o % NG) + ML * (o / NG));
+      const int o = (int)(best & 15u);  // ordinal u * NG + gg: bin = l + T gg + ML u
+      const uint32_t idx = (uint32_t)(lr + T * (o % NG) + ML * (o / NG));
+      const float margin = sqrtf(spec_key_value(best)) - sqrtf(spec_key_value(sec));
+      uint2* mg = reinterpret_cast<uint2*>(a.spec_marg) + f * tot + s;
+      if constexpr (!SYNC) {
+        if (lbest == best && a.syms) a.syms[f * a.sym_stride + (s - 2)] = (uint16_t)idx;
+        if (l == 0) *mg = make_uint2(__float_as_uint(margin), __float_as_uint(pm));
+      } else {
+        if (lbest == best) *mg = make_uint2(__float_as_uint(margin), idx);
       }
-      if (l == 0)
-        reinterpret_cast<float2*>(a.spec_marg)[f * per + j] =
-            make_float2(sqrtf(spec_key_value(best)) - sqrtf(spec_key_value(sec)), pm);
     }
     LORA_STAMP(4, false);
     LORA_STAMP(6, true);
     block_sync<WL>();  // the rows (and red3) are rewritten by the next round
+  };
+  for (int64_t grp = blockIdx.x; grp < groups; grp += gstride) {
+    const int64_t b = grp * BPG + (WL ? wave : 0);  // wave-uniform (workgroup-uniform beyond)
+    if (WL && b >= blocks) break;
+    if (LORA_SPEC_SYNC_FIRST ? b >= blocks - dblocks : b < dblocks)
+      run_block(std::false_type{}, b, grp == blockIdx.x);
+    else
+      run_block(std::true_type{}, b, grp == blockIdx.x);
   }
 }
 
@@ -1151,7 +1167,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   const int tid = threadIdx.x;
   LORA_ESTAMP(5, true);
   LORA_ESTAMP(0, false);
-  if (SPEC == 1 && blockIdx.x == 0 && tid == 0) *a.fix_count = 0;  // the certification's reject list
+  if (SPEC == 1 && blockIdx.x == 0 && tid < kFixStripes) a.fix_count[16 * tid] = 0;  // the reject list
   const int step = DYN ? a.step : N;
   const int osr = DYN ? a.osr : 1;
   const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
@@ -1173,7 +1189,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       // maximum from the demod's (margin, max) pairs, eight loads in flight per lane
       maxv = __uint_as_float(a.maxbits[f]);
       const int per = a.total - 2;
-      const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
+      const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * a.total + 2;
 #pragma unroll 8
       for (int j = l; j < per; j += T) maxv = fmaxf(maxv, mg[j].y);
     } else {
@@ -1396,8 +1412,8 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     }
   }  // exact estimate
   // The sync symbols with the frame's offsets (LoRaDemod.cpp:137-168, 177-192; phy.cpp:
-  // 228-237); in the speculative pipeline only in stage 2, once the exact offsets are known.
-  if constexpr (SPEC != 1) {
+  // 228-237); the speculative pipeline certifies k_spec_demod's instead (below).
+  if constexpr (SPEC == 0) {
     constexpr bool PAIR = EstGeo<SF>::PAIR && MODE <= 1;
     cf in[P], z[P];
     uint32_t sw[2];
@@ -1465,42 +1481,72 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     const FrameParams qs = a.fp_spec[f];
     const int per = a.total - 2;
     const bool same_t = qs.t_off == q.t_off;
+    const double u = 1.0 / 16777216.0;
+    const double E = (8.0 * SF + 32.0) * u;
+    const double drate = fabs((double)q.rate - (double)qs.rate);
+    const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
+    const double tabs = (double)abs(q.t_off);
+    // symbol s certified: its margin d exceeds 4 B (n1 = 2 N x the window's max(|I|,|Q|))
+    auto certified = [&](double d, double wmax, int s) {
+      const double n1 = 2.0 * N * wmax;
+      const double L = (double)(s + 1) * N + tabs;
+      const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
+      const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
+      const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
+      return same_t && d > 4.0 * B;
+    };
+    const uint2* __restrict__ mg = reinterpret_cast<const uint2*>(a.spec_marg) + f * a.total;
+    // the sync symbols (entries 0, 1: margin, index) on lanes 0 and 1: their windows lie in
+    // [0, 2N + t_off), whose maximum the pre-pass took (a.maxbits[f] <= maxv)
+    bool sync_rej = false;
+    {
+      const uint2 e = mg[l < 2 ? l : 0];
+      const bool ok = certified((double)__uint_as_float(e.x), (double)__uint_as_float(a.maxbits[f]), l & 1);
+      const uint32_t ok1 = (uint32_t)__shfl_down((int)ok, 1, 64), i1 = (uint32_t)__shfl_down((int)e.y, 1, 64);
+      if (l == 0 && valid) {
+        if (ok && ok1) {
+          if (a.sync) {
+            const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
+            a.sync[f] = (uint8_t)((((e.y >> shift) & 0x0f) << 4) | ((i1 >> shift) & 0x0f));
+          }
+        } else {
+          sync_rej = true;
+        }
+      }
+    }
     if (valid) {
-      const double u = 1.0 / 16777216.0;
-      const double E = (8.0 * SF + 32.0) * u;
-      const double drate = fabs((double)q.rate - (double)qs.rate);
-      const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
-      const double tabs = (double)abs(q.t_off);
-      const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * per;
-      // the certification tests (eight margin loads in flight per lane), then the rejected
-      // symbols listed for k_spec_fix: one list reservation per wave and round (a -10 dB
-      // batch rejects thousands of symbols; per-lane atomics on one counter serialise)
+      // the data symbols' certification tests (eight margin loads in flight per lane), then
+      // the rejected symbols listed for k_spec_fix: the rounds' ballots first, one list
+      // reservation per wave in the workgroup's stripe (a -10 dB batch rejects thousands of
+      // symbols: per-round or per-lane atomics on one counter serialise); the last round
+      // carries the sync word's entry (data symbol 0xFFFFFFFF)
       uint64_t rejbits = 0;  // bit k: symbol l + T k (per <= kSpecChunks T)
 #pragma unroll 8
       for (int j = l, k = 0; j < per; j += T, ++k) {
-        const float2 v = mg[j];
-        const double n1 = 2.0 * N * (double)v.y;
-        const double L = (double)(3 + j) * N + tabs;
-        const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
-        const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
-        const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
-        if (!(same_t && (double)v.x > 4.0 * B)) rejbits |= 1ull << k;
+        const uint2 v = mg[2 + j];
+        if (!certified((double)__uint_as_float(v.x), (double)__uint_as_float(v.y), 2 + j)) rejbits |= 1ull << k;
       }
       const int rounds = (per + T - 1) / T;  // uniform
-      for (int k = 0; k < rounds; ++k) {
-        const bool rej = (rejbits >> k) & 1;
-        const uint64_t m = __ballot(rej);
-        if (m) {
-          const int lane = (int)__lane_id();
-          const int first = __builtin_ctzll(m);
-          unsigned base = 0;
-          if (lane == first) base = atomicAdd(a.fix_count, (unsigned)__popcll(m));
-          base = (unsigned)__shfl((int)base, first, 64);
+      unsigned total = 0;
+      for (int k = 0; k <= rounds; ++k)
+        total += (unsigned)__popcll(__ballot(k < rounds ? ((rejbits >> k) & 1) != 0 : sync_rej));
+      if (total) {  // wave-uniform
+        const int lane = (int)__lane_id();
+        const int first = __builtin_ctzll(__ballot(1));
+        const int stripe = (int)(blockIdx.x % kFixStripes);
+        unsigned base = 0;
+        if (lane == first) base = atomicAdd(a.fix_count + 16 * stripe, total);
+        base = (unsigned)__shfl((int)base, first, 64);
+        uint32_t* list = a.fix_list + 2 * (size_t)stripe * (size_t)a.fix_cap;
+        for (int k = 0; k <= rounds; ++k) {
+          const bool rej = k < rounds ? ((rejbits >> k) & 1) != 0 : sync_rej;
+          const uint64_t m = __ballot(rej);
           if (rej) {
             const size_t slot = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
-            a.fix_list[2 * slot] = (uint32_t)f;
-            a.fix_list[2 * slot + 1] = (uint32_t)(l + T * k);
+            list[2 * slot] = (uint32_t)f;
+            list[2 * slot + 1] = k < rounds ? (uint32_t)(l + T * k) : 0xFFFFFFFFu;
           }
+          base += (unsigned)__popcll(m);
         }
       }
     }
@@ -1511,7 +1557,9 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
 
 // k_spec_fix: the pipeline's fourth launch.  Every data symbol the certification
 // rejected (k_est_fast<SPEC = 2>'s list: frame, data symbol) recomputed exactly with the
-// frame's exact offsets a.fp[f] (LoRaDemod.cpp:137-175), one T-lane group per symbol, the
+// frame's exact offsets a.fp[f] (LoRaDemod.cpp:137-175), and every rejected sync word
+// (data symbol 0xFFFFFFFF: symbols 0 and 1, LoRaDemod.cpp:177-192), one T-lane group per
+// entry, the
 // list spread over the whole grid - a frame with many rejected symbols no longer holds its
 // certify workgroup while the others idle.  Entry i goes to workgroup i % grid, so a short
 // list still spreads over every CU (slot g of round r: i = blockIdx.x + grid (r SPW + g)).
@@ -1525,18 +1573,48 @@ LORA_SCALAR_FP32 k_spec_fix(KArgs a, int rowc, int64_t grid) {
   const int tid = threadIdx.x;
   const int g = SPW == 1 ? 0 : tid / T;
   const int l = tid % T;
-  const int64_t count = (int64_t)__builtin_nontemporal_load(a.fix_count);
+  // the stripes' counts (every lane loads them: 16 scalar-uniform loads) and their sum
+  int64_t count = 0;
+  unsigned cnt[kFixStripes];
+#pragma unroll
+  for (int t = 0; t < kFixStripes; ++t) {
+    cnt[t] = __builtin_nontemporal_load(a.fix_count + 16 * t);
+    count += cnt[t];
+  }
   if (blockIdx.x == 0 && tid == 0 && count > 0) atomicAdd(a.spec_fix, (unsigned)count);
   cf* row = reinterpret_cast<cf*>(smem) + (size_t)g * rowc;
   for (int64_t r0 = 0; (int64_t)blockIdx.x + grid * r0 < count; r0 += SPW) {  // workgroup-uniform
     const int64_t i = (int64_t)blockIdx.x + grid * (r0 + g);
     const bool valid = i < count;
-    const int64_t k = valid ? i : count - 1;  // spare slots mirror the last entry
-    const int64_t f = a.fix_list[2 * k];
-    const int j = (int)a.fix_list[2 * k + 1];
+    int64_t k = valid ? i : count - 1;  // spare slots mirror the last entry
+    // entry k of the concatenated stripes
+    int t = 0;
+#pragma unroll
+    for (int u = 0; u < kFixStripes - 1; ++u)
+      if (t == u && k >= (int64_t)cnt[u]) {
+        k -= cnt[u];
+        ++t;
+      }
+    const uint32_t* list = a.fix_list + 2 * (size_t)t * (size_t)a.fix_cap;
+    const int64_t f = list[2 * k];
+    const uint32_t j = list[2 * k + 1];
+    const bool sync = j == 0xFFFFFFFFu;  // the sync word: symbols 0 and 1
     const FrameParams q = a.fp[f];
-    const uint32_t idx = exact_symbol<SF, MODE>(a, a.iq + f * a.frame_stride, q, 2 + j, row, l, tid, red);
-    if (l == 0 && valid && a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)idx;
+    const cf* __restrict__ x = a.iq + f * a.frame_stride;
+    const uint32_t i0 = exact_symbol<SF, MODE>(a, x, q, sync ? 0 : 2 + (int)j, row, l, tid, red);
+    // a second transform when any group of the workgroup holds a sync entry (uniform, so
+    // the transform's barriers match); the others repeat theirs
+    const bool any_sync = G::WAVE_LOCAL ? __any(sync) : __syncthreads_or(sync);
+    uint32_t i1 = 0;
+    if (any_sync) i1 = exact_symbol<SF, MODE>(a, x, q, sync ? 1 : 2 + (int)j, row, l, tid, red);
+    if (l == 0 && valid) {
+      if (!sync) {
+        if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)i0;
+      } else if (a.sync) {
+        const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
+        a.sync[f] = (uint8_t)((((i0 >> shift) & 0x0f) << 4) | ((i1 >> shift) & 0x0f));
+      }
+    }
   }
 }
 
@@ -1573,7 +1651,7 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
   const int tid = threadIdx.x;
   LORA_ESTAMP(5, true);
   LORA_ESTAMP(0, false);
-  if (blockIdx.x == 0 && tid == 0) *a.fix_count = 0;  // the certification's reject list
+  if (blockIdx.x == 0 && tid < kFixStripes) a.fix_count[16 * tid] = 0;  // the certification's reject list
   const int g2 = tid / T;     // lane group: frame slot fg, symbol sym
   const int fg = g2 >> 1;
   const int sym = g2 & 1;
@@ -1764,7 +1842,7 @@ bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
   // the kernel's blocks: SPB symbols of one frame (see k_spec_demod), BPG per workgroup round
   constexpr int SPB = G::WAVE_LOCAL ? 64 / G::T : G::SPW, BPG = G::WAVE_LOCAL ? 4 : 1;
   const int per = a.total - 2;
-  const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB);
+  const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB) + (2 * frames + SPB - 1) / SPB;
   const int64_t groups = (blocks + BPG - 1) / BPG;
   const bool persist = LORA_SPEC_PERSIST == 2 || (LORA_SPEC_PERSIST == 1 && G::WAVE_LOCAL);
   const int64_t cap = persist ? (int64_t)device_cus() * LORA_SPEC_WG_PER_CU : groups;
@@ -1785,7 +1863,7 @@ bool launch_spec_fix(const KArgs& a, int64_t frames, hipStream_t st) {
     if (hipFuncSetAttribute((const void*)k_spec_fix<SF, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
       return false;
-  const int64_t most = (frames * (int64_t)(a.total - 2) + G::SPW - 1) / G::SPW;
+  const int64_t most = (frames * (int64_t)(a.total - 1) + G::SPW - 1) / G::SPW;
   const int64_t cap = (int64_t)device_cus() * 2;
   const int64_t grid = std::max<int64_t>(1, std::min(most, cap));
   launch(k_spec_fix<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, rowc, grid);

@@ -13,6 +13,17 @@ constexpr int kMaxBpf = 80;  // SF12 frames of 66 symbols: 66 blocks of 4096 sam
 // symbol; SF6 256, SF7 512, ..., SF12 16384), one certification bit per data symbol in the
 // certify kernel's LDS.
 constexpr int kSpecChunks = 64;
+// The certification's reject list in kFixStripes stripes (stage-2 workgroup b appends to
+// stripe b % kFixStripes): one counter per stripe, 64 bytes apart - a single counter took
+// one returning atomic per wave and round from every workgroup, serialised on one address
+// (about 35 us of the SF7 certify kernel at -10 dB).
+constexpr int kFixStripes = 16;
+// frames per workgroup of the stage-2 kernel (k_est_fast: a T-lane group per frame in
+// blocks of max(T, 64) lanes, T = N/16): the stripes' capacity follows from it
+inline int est_frames_per_block(int N) {
+  const int T = N >= 16 ? N / 16 : 1;
+  return (T >= 64 ? 256 : 64) / T;
+}
 
 struct KArgs {
   const cf* iq;
@@ -47,13 +58,17 @@ struct KArgs {
   // the estimate on unscaled samples, the data symbols' window maxima and certification
   // margins written by the symbol demod, and a device counter of exact recomputations.
   FrameParams* fp_spec = nullptr;  // [frame] estimate on unscaled samples
-  float* spec_marg = nullptr;      // [frame][data symbol][2]: |X1| - |X2|, window max(|I|,|Q|)
+  // [frame][symbol s < total][2]: |X1| - |X2| and, for a data symbol (s >= 2), its window's
+  // max(|I|,|Q|); for a sync symbol (s < 2) the speculative index's bits
+  float* spec_marg = nullptr;
   uint32_t* spec_max = nullptr;    // writable alias of maxbits: [frame] max outside the windows
   unsigned int* spec_fix = nullptr;
-  // the symbols certification rejected, compacted: a count (zeroed by the pre-pass) and
-  // (frame, data symbol) pairs, recomputed exactly by the pipeline's fourth launch
+  // the symbols certification rejected, compacted per stripe: kFixStripes counts (zeroed
+  // by the pre-pass, fix_count[16 s]) and (frame, data symbol) pairs at fix_list[2 (s
+  // fix_cap + i)], recomputed exactly by the pipeline's fourth launch
   unsigned int* fix_count = nullptr;
   uint32_t* fix_list = nullptr;
+  int64_t fix_cap = 0;
 };
 
 // Shape of the fast kernels' LDS passes for SF >= 6 (lora_demod_fast.hip Geo<SF>): pass-1
