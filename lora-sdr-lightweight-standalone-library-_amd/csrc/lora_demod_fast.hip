@@ -914,8 +914,11 @@ __device__ __forceinline__ void stamp(int k, bool real) {
 #ifndef LORA_SPEC_ALIGN
 #define LORA_SPEC_ALIGN 1  // aligned gathers with lane roles (wave-local geometries)
 #endif
-#ifndef LORA_SPEC_SYNC_FIRST
-#define LORA_SPEC_SYNC_FIRST 0  // the sync blocks before the data blocks
+#ifndef LORA_SPEC_RAWSQRT
+#define LORA_SPEC_RAWSQRT 0  // margins from v_sqrt_f32 instead of IEEE sqrtf (A/B)
+#endif
+#ifndef LORA_SPEC_INCDIV
+#define LORA_SPEC_INCDIV 0  // block quotient kept incrementally instead of divided (A/B)
 #endif
 template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
@@ -947,7 +950,8 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   typedef float v2f __attribute__((ext_vector_type(2)));
 
   // one block: SYNC = false a data block (frame-uniform), true a sync block
-  auto run_block = [&](auto sync_c, int64_t b, bool first_round) {
+  // b: the block; data blocks come with b = fb bpf + rb (the loop keeps the quotient)
+  auto run_block = [&](auto sync_c, int64_t b, int64_t fb, int rb, bool first_round) {
     constexpr bool SYNC = decltype(sync_c)::value;
     (void)first_round;  // the diagnostic stamps record a workgroup's first round
     // the lane index, opaque per round: left visible, the compiler hoists every lane
@@ -964,13 +968,12 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     bool valid;
     int rel = 0;    // byte offset of frame f from frame fu
     if constexpr (!SYNC) {
-      if (LORA_SPEC_SYNC_FIRST) b -= blocks - dblocks;
-      f = fu = b / bpf;
-      const int jl = (int)(b - f * bpf) * SPB + gi;
+      f = fu = fb;
+      const int jl = rb * SPB + gi;
       valid = jl < per;
       s = 2 + (valid ? jl : per - 1);  // a partial block's spare slots mirror a valid symbol
     } else {
-      const int64_t k0 = (LORA_SPEC_SYNC_FIRST ? b : b - dblocks) * SPB;
+      const int64_t k0 = (b - dblocks) * SPB;
       int64_t k = k0 + gi;
       valid = k < 2 * frames;
       if (!valid) k = 2 * frames - 1;
@@ -1065,7 +1068,12 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
       const int o = (int)(best & 15u);  // ordinal u * NG + gg: bin = l + T gg + ML u
       const uint32_t idx = (uint32_t)(lr + T * (o % NG) + ML * (o / NG));
-      const float margin = sqrtf(spec_key_value(best)) - sqrtf(spec_key_value(sec));
+      // IEEE sqrtf, or (LORA_SPEC_RAWSQRT) v_sqrt_f32: within 1 ulp, a denormal argument may
+      // give 0 (an absolute error below 2^-63); the certification's E and absolute term
+      // carry either
+      const float margin = LORA_SPEC_RAWSQRT
+                               ? __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec))
+                               : sqrtf(spec_key_value(best)) - sqrtf(spec_key_value(sec));
       uint2* mg = reinterpret_cast<uint2*>(a.spec_marg) + f * tot + s;
       if constexpr (!SYNC) {
         if (lbest == best && a.syms) a.syms[f * a.sym_stride + (s - 2)] = (uint16_t)idx;
@@ -1078,13 +1086,30 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     LORA_STAMP(6, true);
     block_sync<WL>();  // the rows (and red3) are rewritten by the next round
   };
-  for (int64_t grp = blockIdx.x; grp < groups; grp += gstride) {
-    const int64_t b = grp * BPG + (WL ? wave : 0);  // wave-uniform (workgroup-uniform beyond)
+  // b advances by gstride BPG per round: its quotient and remainder by bpf (data blocks)
+  // follow by one scalar add and compare (LORA_SPEC_INCDIV) or a 64-bit division per round
+  const int64_t b0 = (int64_t)blockIdx.x * BPG + (WL ? wave : 0);  // wave-uniform (workgroup-uniform beyond)
+  const int64_t db = gstride * BPG;
+  int64_t fb = b0 / bpf;
+  int rb = (int)(b0 - fb * bpf);
+  const int64_t dq = db / bpf;
+  const int dr = (int)(db - dq * bpf);
+  for (int64_t grp = blockIdx.x, b = b0; grp < groups; grp += gstride, b += db) {
     if (WL && b >= blocks) break;
-    if (LORA_SPEC_SYNC_FIRST ? b >= blocks - dblocks : b < dblocks)
-      run_block(std::false_type{}, b, grp == blockIdx.x);
+    if (!LORA_SPEC_INCDIV) {
+      fb = b / bpf;
+      rb = (int)(b - fb * bpf);
+    }
+    if (b < dblocks)
+      run_block(std::false_type{}, b, fb, rb, grp == blockIdx.x);
     else
-      run_block(std::true_type{}, b, grp == blockIdx.x);
+      run_block(std::true_type{}, b, fb, rb, grp == blockIdx.x);
+    fb += dq;
+    rb += dr;
+    if (rb >= bpf) {
+      rb -= bpf;
+      ++fb;
+    }
   }
 }
 
@@ -1148,6 +1173,87 @@ __device__ __forceinline__ uint32_t exact_symbol(const KArgs& a, const cf* __res
   key = symbol_key<SF>(key, tid, red);
   block_sync<G::WAVE_LOCAL>();  // the row (and red) are rewritten by the next transform
   return key_index(key);
+}
+
+// The certification of a frame's speculative symbols (k_est_fast<SPEC = 2>, k_cert_split):
+// q the frame's exact offsets, LANES lanes per frame (li < LANES this lane's index), the
+// certified sync word written, the rejected symbols listed for k_spec_fix.  Derivation of
+// the bound at k_est_fast<SPEC = 2>.
+template <int SF, int LANES>
+__device__ __forceinline__ void certify_list(const KArgs& a, int64_t f, const FrameParams& q, bool valid, int li) {
+  constexpr int N = 1 << SF;
+  const FrameParams qs = a.fp_spec[f];
+  const int per = a.total - 2;
+  const bool same_t = qs.t_off == q.t_off;
+  const double u = 1.0 / 16777216.0;
+  const double E = (8.0 * SF + 40.0) * u;
+  const double drate = fabs((double)q.rate - (double)qs.rate);
+  const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
+  const double tabs = (double)abs(q.t_off);
+  // symbol s certified: its margin d exceeds 4 B (n1 = 2 N x the window's max(|I|,|Q|))
+  auto certified = [&](double d, double wmax, int s) {
+    const double n1 = 2.0 * N * wmax;
+    const double L = (double)(s + 1) * N + tabs;
+    const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
+    const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
+    const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
+    return same_t && d > 4.0 * B + 0x1p-60;
+  };
+  const uint2* __restrict__ mg = reinterpret_cast<const uint2*>(a.spec_marg) + f * a.total;
+  // the sync symbols (entries 0, 1: margin, index) on lanes 0 and 1: their windows lie in
+  // [0, 2N + t_off), whose maximum the pre-pass took (a.maxbits[f] <= maxv)
+  bool sync_rej = false;
+  {
+    const uint2 e = mg[li < 2 ? li : 0];
+    const bool ok = certified((double)__uint_as_float(e.x), (double)__uint_as_float(a.maxbits[f]), li & 1);
+    const uint32_t ok1 = (uint32_t)__shfl_down((int)ok, 1, 64), i1 = (uint32_t)__shfl_down((int)e.y, 1, 64);
+    if (li == 0 && valid) {
+      if (ok && ok1) {
+        if (a.sync) {
+          const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
+          a.sync[f] = (uint8_t)((((e.y >> shift) & 0x0f) << 4) | ((i1 >> shift) & 0x0f));
+        }
+      } else {
+        sync_rej = true;
+      }
+    }
+  }
+  if (valid) {
+    // the data symbols' certification tests (eight margin loads in flight per lane), then
+    // the rejected symbols listed for k_spec_fix: the rounds' ballots first, one list
+    // reservation per wave in the workgroup's stripe (a -10 dB batch rejects thousands of
+    // symbols: per-round or per-lane atomics on one counter serialise); the last round
+    // carries the sync word's entry (data symbol 0xFFFFFFFF)
+    uint64_t rejbits = 0;  // bit k: symbol li + LANES k (per <= kSpecChunks T)
+#pragma unroll 8
+    for (int j = li, k = 0; j < per; j += LANES, ++k) {
+      const uint2 v = mg[2 + j];
+      if (!certified((double)__uint_as_float(v.x), (double)__uint_as_float(v.y), 2 + j)) rejbits |= 1ull << k;
+    }
+    const int rounds = (per + LANES - 1) / LANES;  // uniform
+    unsigned total = 0;
+    for (int k = 0; k <= rounds; ++k)
+      total += (unsigned)__popcll(__ballot(k < rounds ? ((rejbits >> k) & 1) != 0 : sync_rej));
+    if (total) {  // wave-uniform
+      const int lane = (int)__lane_id();
+      const int first = __builtin_ctzll(__ballot(1));
+      const int stripe = (int)(blockIdx.x % kFixStripes);
+      unsigned base = 0;
+      if (lane == first) base = atomicAdd(a.fix_count + 16 * stripe, total);
+      base = (unsigned)__shfl((int)base, first, 64);
+      uint32_t* list = a.fix_list + 2 * (size_t)stripe * (size_t)a.fix_cap;
+      for (int k = 0; k <= rounds; ++k) {
+        const bool rej = k < rounds ? ((rejbits >> k) & 1) != 0 : sync_rej;
+        const uint64_t m = __ballot(rej);
+        if (rej) {
+          const size_t slot = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
+          list[2 * slot] = (uint32_t)f;
+          list[2 * slot + 1] = k < rounds ? (uint32_t)(li + LANES * k) : 0xFFFFFFFFu;
+        }
+        base += (unsigned)__popcll(m);
+      }
+    }
+  }
 }
 
 #ifndef LORA_EST_WAVES
@@ -1469,87 +1575,18 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     //    (spec_key), moving |X| by < 2^-20 |X|: e_spec = 5 u rmax L + u rmax N + 8e-6;
     //  * the two exact phases differ by |r - r'| L;
     //  * every other rounding (the product y * scale, the rotation product, log2 N
-    //    butterfly stages with table twiddles, |X|^2 and its square root) moves a bin by
-    //    at most E sum_i |y_i| per path, E = (8 log2 N + 32) u (a stage's rounding is
-    //    bounded by its partial sums <= sum_i |y_i|).
+    //    butterfly stages with table twiddles, |X|^2, the demod's v_sqrt_f32 of it - within
+    //    1 ulp - and the margin's subtraction) moves a bin by at most E sum_i |y_i| per path,
+    //    E = (8 log2 N + 40) u (a stage's rounding is bounded by its partial sums <=
+    //    sum_i |y_i|); v_sqrt_f32 may flush a denormal argument to 0, an absolute error
+    //    below 2^-63 that the absolute term 2^-60 of the test covers.
     // With n1 = 2 N max(|re|, |im|) over the window >= sum_i |y_i|, each bin moves by less
     // than B = n1 (|r - r'| L + e_ref + e_spec + 2 E) between the paths, so a speculative
     // top bin ahead of the runner-up by d > 2 B is the reference's argmax, strictly (no
-    // tie to break).  The kernel requires d > 4 B; a symbol that fails is listed and
+    // tie to break).  The kernel requires d > 4 B + 2^-60; a symbol that fails is listed and
     // recomputed exactly with the reference's arithmetic by k_spec_fix, the pipeline's
     // fourth launch, across the whole GPU (lora_demod_spec_recomputed() counts them).
-    const FrameParams qs = a.fp_spec[f];
-    const int per = a.total - 2;
-    const bool same_t = qs.t_off == q.t_off;
-    const double u = 1.0 / 16777216.0;
-    const double E = (8.0 * SF + 32.0) * u;
-    const double drate = fabs((double)q.rate - (double)qs.rate);
-    const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
-    const double tabs = (double)abs(q.t_off);
-    // symbol s certified: its margin d exceeds 4 B (n1 = 2 N x the window's max(|I|,|Q|))
-    auto certified = [&](double d, double wmax, int s) {
-      const double n1 = 2.0 * N * wmax;
-      const double L = (double)(s + 1) * N + tabs;
-      const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
-      const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
-      const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
-      return same_t && d > 4.0 * B;
-    };
-    const uint2* __restrict__ mg = reinterpret_cast<const uint2*>(a.spec_marg) + f * a.total;
-    // the sync symbols (entries 0, 1: margin, index) on lanes 0 and 1: their windows lie in
-    // [0, 2N + t_off), whose maximum the pre-pass took (a.maxbits[f] <= maxv)
-    bool sync_rej = false;
-    {
-      const uint2 e = mg[l < 2 ? l : 0];
-      const bool ok = certified((double)__uint_as_float(e.x), (double)__uint_as_float(a.maxbits[f]), l & 1);
-      const uint32_t ok1 = (uint32_t)__shfl_down((int)ok, 1, 64), i1 = (uint32_t)__shfl_down((int)e.y, 1, 64);
-      if (l == 0 && valid) {
-        if (ok && ok1) {
-          if (a.sync) {
-            const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
-            a.sync[f] = (uint8_t)((((e.y >> shift) & 0x0f) << 4) | ((i1 >> shift) & 0x0f));
-          }
-        } else {
-          sync_rej = true;
-        }
-      }
-    }
-    if (valid) {
-      // the data symbols' certification tests (eight margin loads in flight per lane), then
-      // the rejected symbols listed for k_spec_fix: the rounds' ballots first, one list
-      // reservation per wave in the workgroup's stripe (a -10 dB batch rejects thousands of
-      // symbols: per-round or per-lane atomics on one counter serialise); the last round
-      // carries the sync word's entry (data symbol 0xFFFFFFFF)
-      uint64_t rejbits = 0;  // bit k: symbol l + T k (per <= kSpecChunks T)
-#pragma unroll 8
-      for (int j = l, k = 0; j < per; j += T, ++k) {
-        const uint2 v = mg[2 + j];
-        if (!certified((double)__uint_as_float(v.x), (double)__uint_as_float(v.y), 2 + j)) rejbits |= 1ull << k;
-      }
-      const int rounds = (per + T - 1) / T;  // uniform
-      unsigned total = 0;
-      for (int k = 0; k <= rounds; ++k)
-        total += (unsigned)__popcll(__ballot(k < rounds ? ((rejbits >> k) & 1) != 0 : sync_rej));
-      if (total) {  // wave-uniform
-        const int lane = (int)__lane_id();
-        const int first = __builtin_ctzll(__ballot(1));
-        const int stripe = (int)(blockIdx.x % kFixStripes);
-        unsigned base = 0;
-        if (lane == first) base = atomicAdd(a.fix_count + 16 * stripe, total);
-        base = (unsigned)__shfl((int)base, first, 64);
-        uint32_t* list = a.fix_list + 2 * (size_t)stripe * (size_t)a.fix_cap;
-        for (int k = 0; k <= rounds; ++k) {
-          const bool rej = k < rounds ? ((rejbits >> k) & 1) != 0 : sync_rej;
-          const uint64_t m = __ballot(rej);
-          if (rej) {
-            const size_t slot = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
-            list[2 * slot] = (uint32_t)f;
-            list[2 * slot + 1] = k < rounds ? (uint32_t)(l + T * k) : 0xFFFFFFFFu;
-          }
-          base += (unsigned)__popcll(m);
-        }
-      }
-    }
+    certify_list<SF, T>(a, f, q, valid, l);
     LORA_ESTAMP(7, false);
     LORA_ESTAMP(6, true);
   }
@@ -1635,6 +1672,9 @@ int row_complex() {
 // 28-35 us, its certification state needs the registers - and was removed.
 #ifndef LORA_EST_SPLIT
 #define LORA_EST_SPLIT 1
+#endif
+#ifndef LORA_CERT_SPLIT
+#define LORA_CERT_SPLIT 1  // stage 2 in the same layout (k_cert_split)
 #endif
 template <int SF, int MODE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
@@ -1758,6 +1798,137 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
   }
 }
 
+// k_cert_split<SF, MODE>: stage 2 of the pipeline (k_est_fast<SF, MODE, 2>'s work) for SF
+// 6-9 in k_est_split's layout: symbols 0 and 1 of a frame on two lane groups side by side.
+// Per frame: the maximum assembled from the pre-pass slot and the data windows' maxima
+// (their loads issued together with the group's symbol gather, which does not depend on
+// it), the exact estimate on the normalised samples (LoRaDemod.cpp:59-135; an unscaled
+// frame's is the pre-pass's, recomputed from identical inputs), the outputs, then the
+// certification of every speculative symbol over the frame's 2T lanes (certify_list).
+template <int SF, int MODE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
+LORA_SCALAR_FP32 k_cert_split(KArgs a, int64_t frames, int rowc) {
+  [[maybe_unused]] constexpr int SPEC = 2;  // LORA_ESTAMP's stage
+  using G = Geo<SF>;
+  constexpr int N = G::N, T = G::T, P = G::P;
+  constexpr int FPW = 64 / (2 * T);  // frames per wave (= block)
+  static_assert(2 * T <= 64 && P == 16, "SF 6-9");
+  constexpr bool dech = MODE == 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ FrameParams sp[FPW];
+  __shared__ float tail[FPW][2][4];  // per frame and symbol: index, fractional index, phase, -
+  const int tid = threadIdx.x;
+  LORA_ESTAMP(5, true);
+  LORA_ESTAMP(0, false);
+  const int g2 = tid / T;  // lane group: frame slot fg, symbol sym
+  const int fg = g2 >> 1;
+  const int sym = g2 & 1;
+  const int l = tid % T;          // lane within the group
+  const int l2 = tid % (2 * T);   // lane within the frame's two groups
+  const int64_t f0 = (int64_t)blockIdx.x * FPW + fg;
+  const bool valid = f0 < frames;
+  const int64_t f = valid ? f0 : frames - 1;
+  const cf* __restrict__ x = a.iq + f * a.frame_stride;
+  cf* row = reinterpret_cast<cf*>(smem) + (size_t)g2 * rowc;
+  const int per = a.total - 2;
+  // the group's symbol, dechirped (e2e_chain_test.cpp:88-93), not yet normalised
+  cf in[P], z[P];
+  gather_points<SF>(a, x + (int64_t)sym * N, l, 1, N, 0, 1, dech, 1.0f, in);
+  // LoRaDemod.cpp:59-67 the frame's maximum: the pre-pass's slot (the samples outside the
+  // data windows) and each data window's, over the frame's 2T lanes
+  float maxv = l2 == 0 ? __uint_as_float(a.maxbits[f]) : 0.0f;
+  {
+    const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * a.total + 2;
+#pragma unroll 4
+    for (int j = l2; j < per; j += 2 * T) maxv = fmaxf(maxv, mg[j].y);
+#pragma unroll
+    for (int o = T; o > 0; o >>= 1) maxv = fmaxf(maxv, __shfl_xor(maxv, o, 64));
+  }
+  const int scaled = maxv > 1.0f;
+  const float scale = scaled ? 1.0f / maxv : 1.0f;
+  // LoRaDemod.cpp:68-77 samples * (1/max) after the dechirp (gather_points' order)
+  if (scaled) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) in[q] = cscale(in[q], scale);
+  }
+  LORA_ESTAMP(1, false);
+  // A wave whose frames are all unscaled (max <= 1) takes the pre-pass estimate as it is
+  // (identical inputs and arithmetic); any other computes the exact estimate for all its
+  // frames (an unscaled one's equals the pre-pass's).
+  if (__builtin_amdgcn_readfirstlane(__ballot(scaled) == 0)) {
+    if (l2 == 0) {
+      const FrameParams qs = a.fp_spec[f];
+      sp[fg] = qs;
+      if (valid) {
+        a.fp[f] = qs;
+        if (a.cfo) a.cfo[f] = qs.cfo;
+        if (a.toff) a.toff[f] = qs.toff;
+        if (a.max_amp) a.max_amp[f] = maxv;
+      }
+    }
+  } else {
+    {
+      // LoRaDemod.cpp:79-123 (osr 1: one phase per symbol) for symbol `sym` of the frame
+      rotate_place<SF, false>(in, z, 0.0f, 0.0f, false, a.win, l);
+      uint64_t key = fft_key<SF, true>(z, row, l, a);
+      key = group_max(key, T);
+      if (l == 0) {
+        // LoRaDetector.hpp:60-71 tail on the winning bin, and arg(bin) (LoRaDemod.cpp:124)
+        const uint32_t idx = key_index(key);
+        const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
+        const cf L = row[lds_slot<SF>((int)im1)], R = row[lds_slot<SF>((int)ip1)], B = row[lds_slot<SF>((int)idx)];
+        float pw, fi;
+        detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
+        // best over the (single) osr phase from best_p = -1e30 (LoRaDemod.cpp:86-101)
+        const bool take = pw > -1e30f;
+        tail[fg][sym][0] = take ? (float)idx : 0.0f;
+        tail[fg][sym][1] = take ? fi : 0.0f;
+        tail[fg][sym][2] = lm_atan2f(take ? B.im : 0.0f, take ? B.re : 0.0f);
+      }
+      wave_sync();
+    }
+    LORA_ESTAMP(2, false);
+    if (l2 == 0) {
+      // LoRaDemod.cpp:105-135 in the reference's order: symbol 0's terms, then symbol 1's
+      float sum_index = 0.0f, phase_diff = 0.0f;
+      sum_index += tail[fg][0][0] + tail[fg][0][1];
+      sum_index += tail[fg][1][0] + tail[fg][1][1];
+      float d = tail[fg][1][2] - tail[fg][0][2];
+      while (d > PI_F) d -= 2.0f * PI_F;
+      while (d < -PI_F) d += 2.0f * PI_F;
+      phase_diff += d;
+      const float avg_index = sum_index / 2.0f;
+      const float cfo_coarse = avg_index / (float)N;
+      const float cfo_fine = (phase_diff / 1.0f) / (2.0f * PI_F * (float)N);
+      const float cfo = cfo_coarse + cfo_fine;
+      const float frac = avg_index - floorf(avg_index + 0.5f);
+      const float avg_t = (float)0u / 2.0f;
+      const float toff = avg_t - frac * (float)N * 1.0f;
+      FrameParams qe;
+      qe.cfo = cfo;
+      qe.toff = toff;
+      qe.t_off = (int)roundf(toff);
+      qe.rate = -2.0f * PI_F * cfo / (float)N;
+      qe.scale = scale;
+      qe.scaled = scaled;
+      qe.pad0 = qe.pad1 = 0;
+      sp[fg] = qe;
+      if (valid) {
+        a.fp[f] = qe;
+        if (a.cfo) a.cfo[f] = cfo;
+        if (a.toff) a.toff[f] = toff;
+        if (a.max_amp) a.max_amp[f] = maxv;
+      }
+    }
+  }
+  wave_sync();
+  const FrameParams q = sp[fg];
+  LORA_ESTAMP(3, false);
+  certify_list<SF, 2 * T>(a, f, q, valid, l2);
+  LORA_ESTAMP(7, false);
+  LORA_ESTAMP(6, true);
+}
+
 template <int SF, int MODE>
 bool launch_est_split(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
@@ -1769,6 +1940,17 @@ bool launch_est_split(const KArgs& a, int64_t frames, hipStream_t st) {
   return true;
 }
 
+
+template <int SF, int MODE>
+bool launch_cert_split(const KArgs& a, int64_t frames, hipStream_t st) {
+  using G = Geo<SF>;
+  constexpr int FPW = 64 / (2 * G::T);
+  const int rowc = row_complex<SF>();
+  const size_t lds = sizeof(cf) * (size_t)(2 * FPW) * rowc;
+  const int64_t grid = (frames + FPW - 1) / FPW;
+  launch(k_cert_split<SF, MODE>, dim3((unsigned)grid), dim3(64), lds, st, a, frames, rowc);
+  return true;
+}
 
 template <int SF, int MODE, int SPEC = 0>
 bool launch_est_mode(const KArgs& a, int64_t frames, hipStream_t st) {
@@ -1878,6 +2060,8 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   } else {
     if constexpr (SF <= 9 && LORA_EST_SPLIT) {
       if (stage == 0) return a.dechirp ? launch_est_split<SF, 0>(a, frames, st) : launch_est_split<SF, 1>(a, frames, st);
+      if (stage == 2 && LORA_CERT_SPLIT)
+        return a.dechirp ? launch_cert_split<SF, 0>(a, frames, st) : launch_cert_split<SF, 1>(a, frames, st);
     }
     if (stage == 3) return a.dechirp ? launch_spec_fix<SF, 0>(a, frames, st) : launch_spec_fix<SF, 1>(a, frames, st);
     if (stage == 0) return a.dechirp ? launch_est_mode<SF, 0, 1>(a, frames, st) : launch_est_mode<SF, 1, 1>(a, frames, st);
