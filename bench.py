@@ -247,9 +247,13 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     # write, plus 9 B of per-frame outputs
     step_bytes = frames * (total_syms * B_sym + 9)
     # the dominant kernel's own algorithmic bytes per launch
+    # (the speculative pipeline's symbol pass also demodulates the sync symbols: every
+    # window of the frame read once, one index written per data symbol)
+    spec = "spec" in kernels
     dom_bytes = {0: frames * total_syms * 8 * N,             # frame max: the whole IQ
                  1: frames * (2 * 8 * N + 9),                 # estimate: symbols 0/1 + outputs
-                 2: frames * data_syms * B_sym}[dom]          # demod: data symbols
+                 2: (frames * (total_syms * 8 * N + 2 * data_syms) if spec
+                     else frames * data_syms * B_sym)}[dom]   # demod
     dom_gbs = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9
     return {
         "sf": sf, "frames": frames, "data_symbols": frames * data_syms, "iq_bytes": iq.numel() * 8,
@@ -489,6 +493,11 @@ def roofline(r, probe=None):
             "traffic": pmc_dom,
             "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch, "
                               "tools/pmc_r03.py; committed, not measured in this run)",
+            # the kernel's other roof: VALU issue (SQ_INSTS_VALU x 4 cycles over 1024 SIMDs x the
+            # GRBM-measured cycles of the same launch, committed profile)
+            "valu": {"busy_frac": load_pmc(wl, "valu_busy_frac"),
+                     "instr_per_symbol": load_pmc(wl, "valu_instr_per_symbol"),
+                     "source": "profiles/pmc_summary.json (rocprofv3 SQ_INSTS_VALU, GRBM_GUI_ACTIVE)"},
             "pipeline": {"algorithmic_bytes_per_step": r["step_bytes"], "ms_per_step": r["ms_per_step"],
                          "achieved": r["pipeline_gbs"], "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS,
                          "counter_bytes_per_step": pmc_step,

@@ -45,7 +45,9 @@ for wl, (sf, frames, S) in WL.items():
     fe = per_kernel(os.path.join(src, f"pmc_fetch{sf}"), "FETCH_SIZE")
     wr = per_kernel(os.path.join(src, f"pmc_write{sf}"), "WRITE_SIZE")
     N = 1 << sf
-    algo = {"k_spec_demod": frames * S * (8 * N + 2)}
+    # the symbol pass reads every symbol's window (the sync symbols' too) and writes one
+    # u16 index per data symbol
+    algo = {"k_spec_demod": frames * ((S + 2) * 8 * N + 2 * S)}
     step = 0.0
     d = {"step_kernels": {}}
     for k in sorted(fe):
@@ -73,6 +75,24 @@ for wl, (sf, frames, S) in WL.items():
             d[key] = d[key] * scale
     summary[wl] = d
     lines.append(f"| {wl} | whole step | | | | {step:.4g} | {step_algo:.4g} | {step / step_algo:.4f} |")
+# VALU issue of the symbol pass from the SQ passes (tools/r03_final.sh: pmc1/pmc2 hold
+# SQ_INSTS_VALU, pmc5/pmc6 GRBM_GUI_ACTIVE for sf7/sf12): a wave64 VALU instruction occupies
+# its SIMD 4 cycles; GRBM_GUI_ACTIVE sums the XCDs' busy cycles.
+SIMDS, XCDS = 1024, 8
+lines += ["", "## VALU issue of the symbol pass", "",
+          "| workload | kernel | VALU wave-instr / launch | GPU cycles / launch (per XCD) | clock GHz (trace) | VALU busy |",
+          "|---|---|---:|---:|---:|---:|"]
+for wl, (sf, frames, S), (pv, pg) in zip(WL, WL.values(), (("pmc1", "pmc5"), ("pmc2", "pmc6"))):
+    vi = per_kernel(os.path.join(src, pv), "SQ_INSTS_VALU")
+    gr = per_kernel(os.path.join(src, pg), "GRBM_GUI_ACTIVE")
+    k = summary[wl].get("kernel")
+    if not k or k not in vi or k not in gr:
+        continue
+    cyc = gr[k] / XCDS
+    busy = vi[k] * 4 / (SIMDS * cyc)
+    summary[wl].update({"valu_instr_per_launch": vi[k], "gpu_cycles_per_launch": cyc, "valu_busy_frac": busy,
+                        "valu_instr_per_symbol": vi[k] / (frames * (S + 2))})
+    lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | | {busy:.3f} |")
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 open(dst, "w").write("\n".join(lines) + "\n")
 json.dump(summary, open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w"), indent=1)
