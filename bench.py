@@ -192,7 +192,7 @@ def stage_times(plan, iq, out, steps, device):
 
 
 def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, precision="exact",
-               inputs=None, sync=None, seed_base=20251015, rank=0):
+               inputs=None, sync=None, seed_base=20251015, rank=0, window="none"):
     import torch
 
     import lora_phy_amd as amd
@@ -200,7 +200,7 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     N = 1 << sf
     syms, iq = inputs if inputs is not None else make_input(sf, frames, data_syms, seed_base + rank, device,
                                                             snr_db, sync)
-    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device,
+    plan = amd.DemodPlan(sf, 1, 125000, window, dechirp=True, mode="legacy", device=device,
                          precision=precision)
     out = None
     for _ in range(warmup):
@@ -585,6 +585,12 @@ def main():
         extra["awgn_m10db_sf7"] = variant_summary(rn, r7, "AWGN -10 dB: symbol errors and near-ties; symbols "
                                                          "failing certification are recomputed exactly")
         del rn
+        # the Hann window (LoRaDemod.cpp:158-160) on the headline batch
+        rh = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, window="hann",
+                        inputs=(r7["syms"], r7["iq"]), rank=rank)
+        extra["hann_sf7"] = variant_summary(rh, r7, "Hann window, same batch (ser_vs_tx: the window's own "
+                                                    "effect on the reference's decisions, not an error)")
+        del rh
         # a 255-byte payload: 510 data symbols per frame (lora_encode: 2 symbols per byte)
         long_frames = max(1, args.frames * args.data_symbols // 510)
         rl = run_config(7, long_frames, 510, args.steps, args.warmup, dist, device, rank=rank)

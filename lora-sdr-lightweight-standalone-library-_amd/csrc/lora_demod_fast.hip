@@ -937,7 +937,7 @@ __device__ __forceinline__ void stamp(int k, bool real) {
 #ifndef LORA_SPEC_RAWSQRT
 #define LORA_SPEC_RAWSQRT 1  // margins from v_sqrt_f32 instead of IEEE sqrtf (-0.5 %)
 #endif
-template <int SF, int MODE>
+template <int SF, int MODE, bool HANN = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   using G = Geo<SF>;
@@ -1069,7 +1069,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     LORA_STAMP(1, false);
     const float start = rate * ((float)((uint32_t)s * (uint32_t)N) + (float)toff);
     cf z[P];
-    rotate_place<SF, true, true, true>(in, z, start, rate, false, a.win, lr);
+    rotate_place<SF, true, true, true>(in, z, start, rate, HANN, a.win, lr);
     asm volatile("" : "+v"(pm));
     LORA_STAMP(2, false);
     const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true>(z, rows + (size_t)g * rowc, lr, a, nullptr, twl);
@@ -1198,7 +1198,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       asm volatile("" : "+v"(pm));
       const float start = B.rate * ((float)((uint32_t)B.s * (uint32_t)N) + (float)B.toff);
       cf z[P];
-      rotate_place<SF, true, true, true>(in, z, start, B.rate, false, a.win, lr);
+      rotate_place<SF, true, true, true>(in, z, start, B.rate, HANN, a.win, lr);
       asm volatile("" : "+v"(pm));
       // the next block's samples, requested once this block's are consumed (their registers
       // are free again)
@@ -1291,7 +1291,7 @@ __device__ __forceinline__ uint32_t exact_symbol(const KArgs& a, const cf* __res
   const int osr = DYN ? a.osr : 1;
   const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
   const bool dech = DYN ? (legacy && a.dechirp) : (MODE == 0);
-  const bool hann = DYN ? (a.hann != 0) : false;
+  const bool hann = a.hann != 0;  // MODE 0/1: only the pipeline's frames may be windowed
   int64_t base;
   int cg;
   sym_base(s, step, a.frame_len, q.t_off, base, cg);
@@ -1316,7 +1316,7 @@ __device__ __forceinline__ void certify_list(const KArgs& a, int64_t f, const Fr
   const int per = a.total - 2;
   const bool same_t = qs.t_off == q.t_off;
   const double u = 1.0 / 16777216.0;
-  const double E = (8.0 * SF + 40.0) * u;
+  const double E = (8.0 * SF + 42.0) * u;
   const double drate = fabs((double)q.rate - (double)qs.rate);
   const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
   const double tabs = (double)abs(q.t_off);
@@ -1408,7 +1408,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   const int osr = DYN ? a.osr : 1;
   const bool legacy = DYN ? a.mode != LORA_MODE_API : true;
   const bool dech = DYN ? (legacy && a.dechirp) : (MODE == 0);
-  const bool hann = DYN ? (a.hann != 0) : false;
+  const bool hann = (DYN || SPEC != 0) ? (a.hann != 0) : false;  // the pipeline's frames may be windowed
   const int g = tid / T;
   const int l = tid % T;
   const int64_t f0 = (int64_t)blockIdx.x * SPB + g;
@@ -1705,9 +1705,9 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     //    (spec_key), moving |X| by < 2^-20 |X|: e_spec = 5 u rmax L + u rmax N + 8e-6;
     //  * the two exact phases differ by |r - r'| L;
     //  * every other rounding (the product y * scale, the rotation product, log2 N
-    //    butterfly stages with table twiddles, |X|^2, the demod's v_sqrt_f32 of it - within
-    //    1 ulp - and the margin's subtraction) moves a bin by at most E sum_i |y_i| per path,
-    //    E = (8 log2 N + 40) u (a stage's rounding is bounded by its partial sums <=
+    //    butterfly stages with table twiddles, a Hann window's product (|w| <= 1), |X|^2, the
+    //    demod's v_sqrt_f32 of it - within 1 ulp - and the margin's subtraction) moves a bin
+    //    by at most E sum_i |y_i| per path, E = (8 log2 N + 42) u (a stage's rounding is bounded by its partial sums <=
     //    sum_i |y_i|); v_sqrt_f32 may flush a denormal argument to 0, an absolute error
     //    below 2^-63 that the absolute term 2^-60 of the test covers.
     // With n1 = 2 N max(|re|, |im|) over the window >= sum_i |y_i|, each bin moves by less
@@ -1852,7 +1852,7 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
 #pragma unroll
     for (int k = 0; k < P; ++k) mo = amax3(mo, in[k]);
     asm volatile("" : "+v"(mo));
-    rotate_place<SF, false>(in, z, 0.0f, 0.0f, false, a.win, l);
+    rotate_place<SF, false>(in, z, 0.0f, 0.0f, a.hann != 0, a.win, l);
     uint64_t key = fft_key<SF, true>(z, row, l, a);
     key = group_max(key, T);
     if (l == 0) {
@@ -1999,7 +1999,7 @@ LORA_SCALAR_FP32 k_cert_split(KArgs a, int64_t frames, int rowc) {
   } else {
     {
       // LoRaDemod.cpp:79-123 (osr 1: one phase per symbol) for symbol `sym` of the frame
-      rotate_place<SF, false>(in, z, 0.0f, 0.0f, false, a.win, l);
+      rotate_place<SF, false>(in, z, 0.0f, 0.0f, a.hann != 0, a.win, l);
       uint64_t key = fft_key<SF, true>(z, row, l, a);
       key = group_max(key, T);
       if (l == 0) {
@@ -2141,14 +2141,14 @@ int device_cus() {
   return cache[dev];
 }
 
-template <int SF, int MODE>
-bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
+template <int SF, int MODE, bool HANN>
+bool launch_spec_demod_w(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
   const size_t lds = sizeof(cf) * ((size_t)G::SPW * rowc + demod_twl_entries<SF, true>());
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
       return false;
   // the kernel's blocks: SPB symbols of one frame (see k_spec_demod), BPG per workgroup round
@@ -2159,8 +2159,14 @@ bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
   const bool persist = LORA_SPEC_PERSIST == 2 || (LORA_SPEC_PERSIST == 1 && G::WAVE_LOCAL);
   const int64_t cap = persist ? (int64_t)device_cus() * LORA_SPEC_WG_PER_CU : groups;
   const int64_t grid = groups < cap ? groups : cap;
-  launch(k_spec_demod<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
+  launch(k_spec_demod<SF, MODE, HANN>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
   return true;
+}
+// the Hann window (LoRaDemod.cpp:158-160) as an instantiation of its own: the unwindowed
+// kernels keep no per-point branch
+template <int SF, int MODE>
+bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
+  return a.hann ? launch_spec_demod_w<SF, MODE, true>(a, frames, st) : launch_spec_demod_w<SF, MODE, false>(a, frames, st);
 }
 
 // k_spec_fix's grid: two workgroups per CU (or fewer when the frames hold fewer data

@@ -86,8 +86,8 @@ CASES = [  # (sf, osr, hann, dechirp, F, symbols-per-frame, extra samples, kind)
 
 def make_plan(amd, path, *args, **kw):
     """path "fast": the default - register-blocked kernels, as the speculative single-read
-    pipeline wherever it covers the configuration (LEGACY, osr 1, no window, SF >= 6,
-    >= 3 symbols); "split": the same kernels as three launches (frame max, estimate,
+    pipeline wherever it covers the configuration (LEGACY, osr 1, SF >= 6,
+    >= 3 symbols, either window); "split": the same kernels as three launches (frame max, estimate,
     demod: LORA_MI355X_SPEC=0, the one diagnostic knob)."""
     import os
 

@@ -336,3 +336,40 @@ def test_fused_dechirp_large_cfo_and_delay(O, amd, sf, S, F, snr_db):
         assert bits(res.time_offset[f].item()) == bits(otoff)
         nz += otoff != 0
     assert nz > 0, "no frame exercised a non-zero time offset"
+
+
+@pytest.mark.parametrize("sf,S,F,dechirp", [(6, 40, 16, True), (7, 66, 24, True), (7, 20, 12, False),
+                                            (9, 30, 6, True), (10, 12, 4, False), (12, 8, 3, True)])
+@pytest.mark.parametrize("snr_db", [20, -5])
+def test_hann_window_through_the_pipeline(O, amd, sf, S, F, dechirp, snr_db):
+    """Hann-windowed frames (LoRaDemod.cpp:88-92, 158-160: the window multiplies every
+    sample after the rotation, in the estimate and in the symbol loop) take the speculative
+    pipeline (the window's product is one more rounding in the certification bound, |w| <= 1
+    keeps the bound's n1): carrier offsets up to +-0.45 bin and random delays (t_off != 0),
+    against the oracle bit for bit, fused caller dechirp and dechirped input."""
+    N = 1 << sf
+    rng = np.random.default_rng(9100 + 10 * sf + snr_db + S)
+    L = S * N
+    iq = np.zeros((F, L), np.complex64)
+    for f in range(F):
+        syms = rng.integers(0, N, S - 2).astype(np.uint16)
+        x = O.lora_modulate(syms, sf, 1, 125000, 1.0, int(rng.integers(0, 256))).astype(np.complex128)
+        x = x * np.exp(2j * np.pi * rng.uniform(-0.45, 0.45) * np.arange(len(x)) / N)
+        d = int(rng.integers(0, N // 3))
+        x = np.concatenate([np.zeros(d), x])[:L]
+        amp = rng.uniform(0.7, 1.5)
+        sigma = amp * 10 ** (-snr_db / 20) / np.sqrt(2)
+        x = amp * x + sigma * (rng.standard_normal(L) + 1j * rng.standard_normal(L))
+        iq[f] = x.astype(np.complex64)
+    plan = amd.DemodPlan(sf, 1, 125000, "hann", dechirp=dechirp)
+    res = plan.run(torch.from_numpy(iq).cuda())
+    torch.cuda.synchronize()
+    assert "spec" in plan.last_kernels()
+    syms = res.symbols.cpu().numpy()
+    for f in range(F):
+        xd = O.dechirp(iq[f], sf, 1) if dechirp else iq[f]
+        osym, osync, ocfo, otoff = O.lora_demodulate(xd, sf, 1, True)
+        np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
+        assert int(res.sync[f]) == osync, f"frame {f} sync"
+        assert bits(res.cfo[f].item()) == bits(ocfo), f"frame {f} cfo"
+        assert bits(res.time_offset[f].item()) == bits(otoff), f"frame {f} toff"

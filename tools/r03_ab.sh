@@ -17,7 +17,7 @@ import json, sys
 d = json.load(open(sys.argv[1])); e = d["extra"]
 r = lambda x: round(x, 4)
 line = [sys.argv[2], "sf7", r(d["ms_per_step"]), [r(x) for x in d["config"]["stage_ms"][1:]]]
-for k in ("awgn_m10db_sf7", "awgn_0db_sf7", "sync_ff_sf7", "long_frames_sf7", "sf12", "awgn_m10db_sf12"):
+for k in ("awgn_m10db_sf7", "awgn_0db_sf7", "sync_ff_sf7", "hann_sf7", "long_frames_sf7", "sf12", "awgn_m10db_sf12"):
     if k in e:
         line += [k, r(e[k]["ms_per_step"]), [r(x) for x in e[k].get("stage_ms", [0, 0, 0])[1:]]]
 print(*line, flush=True)
