@@ -1009,7 +1009,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     // wave-uniform frame base: the point offsets T q (up to 30 KB at SF12) go in the scalar
     // offset or the immediate, not in 64-bit vector adds.  Byte offsets fit 31 bits: the
     // pipeline's frames hold < 2^26 samples.
-    // Alignment (wave-local geometries): a load instruction fetches T consecutive samples
+    // Alignment: a load instruction fetches T consecutive samples
     // per symbol; a window at base = A + d (A a multiple of D = min(T, 8) samples, so the
     // chunks never straddle a 128-byte line: one straddling in two cost the SF7 demod 19 %)
     // is read from A instead, and lane l plays the role lr = (l - d) mod T of the FFT: its
@@ -1017,7 +1017,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     // the lane takes 17 loads and selects.  The roles permute the lanes of each symbol, so
     // the LDS accesses (and their banks) of every instruction are the same set.
     constexpr int D = T < 8 ? T : 8;
-    constexpr bool AL = WL && LORA_SPEC_ALIGN;
+    constexpr bool AL = LORA_SPEC_ALIGN;
     const int d = AL ? (int)(base & (D - 1)) : 0;
     const int lr = AL ? ((l - d) & (T - 1)) : l;
     v2f ld[P + 1];
@@ -1039,7 +1039,8 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       for (int q = 2 * pp; q < 2 * pp + 2; ++q)
         ld[q] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
     }
-    if (AL && __builtin_amdgcn_readfirstlane(__ballot(d != 0) != 0)) {
+    // (only waves holding a lane l < d: for T > 64 the symbol's first wave)
+    if (AL && __builtin_amdgcn_readfirstlane(__ballot(l < d) != 0)) {
       // the 17th load: lanes l < d take window points; the others (whose load would fall up
       // to T samples past the window, possibly past the batch) re-read load 15's sample
       const bool late = l < d;
