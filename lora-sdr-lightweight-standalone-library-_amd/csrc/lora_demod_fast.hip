@@ -1861,10 +1861,10 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
       const uint32_t idx = key_index(key);
       const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
       const cf L = row[lds_slot<SF>((int)im1)], R = row[lds_slot<SF>((int)ip1)], B = row[lds_slot<SF>((int)idx)];
-      float pw, fi;
-      detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
-      // best over the (single) osr phase from best_p = -1e30 (LoRaDemod.cpp:86-101)
-      const bool take = pw > -1e30f;
+      // best over the (single) osr phase from best_p = -1e30 (LoRaDemod.cpp:86-101):
+      // taken exactly when |X|^2 > 0 (detect_findex)
+      const float fi = detect_findex(key_value(key), L, R);
+      const bool take = key_value(key) > 0.0f;
       tail[fg][sym][0] = take ? (float)idx : 0.0f;
       tail[fg][sym][1] = take ? fi : 0.0f;
       tail[fg][sym][2] = lm_atan2f(take ? B.im : 0.0f, take ? B.re : 0.0f);
@@ -2008,10 +2008,10 @@ LORA_SCALAR_FP32 k_cert_split(KArgs a, int64_t frames, int rowc) {
         const uint32_t idx = key_index(key);
         const uint32_t im1 = idx > 0 ? idx - 1 : N - 1, ip1 = idx < (uint32_t)N - 1 ? idx + 1 : 0;
         const cf L = row[lds_slot<SF>((int)im1)], R = row[lds_slot<SF>((int)ip1)], B = row[lds_slot<SF>((int)idx)];
-        float pw, fi;
-        detect_tail(key_value(key), L, R, a.power_scale, &pw, &fi);
-        // best over the (single) osr phase from best_p = -1e30 (LoRaDemod.cpp:86-101)
-        const bool take = pw > -1e30f;
+        // best over the (single) osr phase from best_p = -1e30 (LoRaDemod.cpp:86-101):
+        // taken exactly when |X|^2 > 0 (detect_findex)
+        const float fi = detect_findex(key_value(key), L, R);
+        const bool take = key_value(key) > 0.0f;
         tail[fg][sym][0] = take ? (float)idx : 0.0f;
         tail[fg][sym][1] = take ? fi : 0.0f;
         tail[fg][sym][2] = lm_atan2f(take ? B.im : 0.0f, take ? B.re : 0.0f);
@@ -2170,7 +2170,7 @@ bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
   return a.hann ? launch_spec_demod_w<SF, MODE, true>(a, frames, st) : launch_spec_demod_w<SF, MODE, false>(a, frames, st);
 }
 
-// k_spec_fix's grid: two workgroups per CU (or fewer when the frames hold fewer data
+// k_spec_fix's grid: one workgroup per CU (or fewer when the frames hold fewer data
 // symbols); it reads the list's length on the device, so the launch does not wait for it.
 template <int SF, int MODE>
 bool launch_spec_fix(const KArgs& a, int64_t frames, hipStream_t st) {
@@ -2183,7 +2183,7 @@ bool launch_spec_fix(const KArgs& a, int64_t frames, hipStream_t st) {
                             (int)lds) != hipSuccess)
       return false;
   const int64_t most = (frames * (int64_t)(a.total - 1) + G::SPW - 1) / G::SPW;
-  const int64_t cap = (int64_t)device_cus() * 2;
+  const int64_t cap = (int64_t)device_cus();  // (one per CU: an empty list costs a smaller ramp)
   const int64_t grid = std::max<int64_t>(1, std::min(most, cap));
   launch(k_spec_fix<SF, MODE>, dim3((unsigned)grid), dim3(256), lds, st, a, rowc, grid);
   return true;

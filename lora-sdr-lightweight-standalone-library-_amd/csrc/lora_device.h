@@ -159,6 +159,18 @@ __device__ __forceinline__ uint64_t group_max(uint64_t k, int T) {
   return k;
 }
 
+// LoRaDetector.hpp:66-71: the fractional index alone.  Single-phase estimates (osr 1) use
+// the power only through LoRaDemod.cpp:97's `p > best_p` against best_p = -1e30, which
+// holds exactly when fund2 > 0 (20 log10(sqrt(fund2)) - power_scale is finite for every
+// positive fund2, -inf for 0, NaN for NaN), so they skip the log10f.
+__device__ __forceinline__ float detect_findex(float fund2, cf L, cf R) {
+  const float fundamental = sqrtf(fund2);
+  const float left = lm_hypotf(L.re, L.im);
+  const float right = lm_hypotf(R.re, R.im);
+  const double demon = (2.0 * (double)fundamental) - (double)right - (double)left;
+  return demon == 0.0 ? 0.0f : (float)(0.5 * (double)(right - left) / demon);
+}
+
 // LoRaDetector.hpp:60-71 for the winning bin: power p and fractional index.
 // `fund2` = max |X|^2, `L`/`R` = the neighbour bins (wrap-around).
 __device__ __forceinline__ void detect_tail(float fund2, cf L, cf R, float power_scale,
