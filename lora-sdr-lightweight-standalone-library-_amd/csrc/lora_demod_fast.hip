@@ -1159,9 +1159,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     if (b < dblocks) issue(b, nb);
     for (; b < dblocks; b += gstride * BPG, grp0 += gstride) {
       const Blk B = nb;
-      v2f ld[P + 1];
-#pragma unroll
-      for (int q = 0; q <= P; ++q) ld[q] = nx[q];
+      v2f(&ld)[P + 1] = nx;  // this block's samples, consumed in place (no copy per round)
       const int d = B.d;
       const int lr = (l - d) & (T - 1);
       // this block's table pairs and pass 1's twiddles, then the next block's samples
