@@ -24,8 +24,10 @@ def _run(args, env=None):
 def test_bench_forms_n_ranks(n):
     p = _run(["--gpus", str(n), "--plumbing"])
     assert p.returncode == 0, p.stderr
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, p.stdout  # one JSON line, from rank 0 only
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    # stdout is exactly one JSON line, from rank 0 only (gloo's connection reports go to
+    # stderr: the driver parses the job's stdout)
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == n
     assert [r["rank"] for r in d["ranks"]] == list(range(n))
