@@ -106,7 +106,9 @@ void release(device_state& d);
 }  // namespace detail
 
 /* phy.hpp:77-92 (same name and caller-visible fields; device state instead of kissfft
- * plans).  Released by its destructor: the reference's workspace API has no free call. */
+ * plans).  Released by its destructor: the reference's workspace API has no free call.
+ * Lifetime: destroy it while the HIP runtime is alive (before exit's static destructors); a
+ * workspace destroyed after the runtime's teardown skips the release (hipGetDevice fails). */
 struct lora_workspace {
   uint16_t* symbol_buf{};
   std::complex<float>* fft_in{};

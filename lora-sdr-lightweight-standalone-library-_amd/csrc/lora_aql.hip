@@ -60,6 +60,7 @@ struct AqlQueue {
   AqlKernel k[kCache];
   int nk = 0;
   bool hsa_up = false;
+  bool broken = false;  // a call timed out with work in flight (aql_run refuses, -63)
 };
 
 namespace {
@@ -160,7 +161,9 @@ const AqlKernel* kernel_of(AqlQueue* Q, const void* fn) {
 // The gfx950 code objects of the clang offload bundles in this library's .hip_fatbin
 // section (uncompressed bundles: "__CLANG_OFFLOAD_BUNDLE__", an entry count, then per
 // entry offset, size, triple length and triple).
-bool own_code_objects(std::vector<unsigned char>& file, std::vector<std::pair<size_t, size_t>>& objs) {
+bool own_code_objects(std::vector<unsigned char>& file, std::vector<std::pair<size_t, size_t>>& objs,
+                      bool& compressed) {
+  compressed = false;
   Dl_info info{};
   if (!dladdr(reinterpret_cast<void*>(&aql_create), &info) || !info.dli_fname) return false;
   FILE* fp = std::fopen(info.dli_fname, "rb");
@@ -185,6 +188,8 @@ bool own_code_objects(std::vector<unsigned char>& file, std::vector<std::pair<si
     static const char kMagic[] = "__CLANG_OFFLOAD_BUNDLE__";
     const size_t lo = sh[i].sh_offset, hi = lo + sh[i].sh_size;
     for (size_t pos = lo; pos + 32 <= hi; pos += 8) {  // bundles start 8-byte aligned
+      // a compressed bundle ("CCOB", --offload-compress) is not parsed: aql_create reports it
+      if (std::memcmp(file.data() + pos, "CCOB", 4) == 0) compressed = true;
       if (std::memcmp(file.data() + pos, kMagic, 24) != 0) continue;
       uint64_t cnt;
       std::memcpy(&cnt, file.data() + pos + 24, 8);
@@ -270,8 +275,9 @@ int aql_create(int device, AqlQueue** out) {
     // this library's gfx950 code objects, loaded for the agent
     std::vector<unsigned char> file;
     std::vector<std::pair<size_t, size_t>> objs;
-    if (!own_code_objects(file, objs) || objs.size() > (size_t)kMaxExec) {
-      rc = -103;
+    bool compressed = false;
+    if (!own_code_objects(file, objs, compressed) || objs.size() > (size_t)kMaxExec) {
+      rc = objs.empty() && compressed ? -111 : -103;  // -111: built with --offload-compress
       break;
     }
     for (const auto& o : objs) {
@@ -308,6 +314,9 @@ int aql_create(int device, AqlQueue** out) {
 
 void aql_destroy(AqlQueue* Q) {
   if (!Q) return;
+  // a queue whose kernels may still be running is left as it is (leaked): destroying it would
+  // free the kernarg slots and the signal under them
+  if (Q->broken) return;
   if (Q->done.handle) hsa_signal_destroy(Q->done);
   if (Q->q) hsa_queue_destroy(Q->q);
   if (Q->kernarg) hsa_amd_memory_pool_free(Q->kernarg);
@@ -332,11 +341,13 @@ int aql_run(AqlQueue* Q, const LaunchRecord& r) {
     if (ks[i]->kernarg > kSlotBytes || (uint64_t)r.l[i].grid * r.l[i].block > 0xffffffffull) return -22;
   }
   hsa_queue_t* q = Q->q;
+  // Every call waits for its last packet, so the queue is idle here - unless an earlier call
+  // timed out with packets still queued or running: their kernarg slots, staging and
+  // completion signal must not be reused, so refuse before writing anything (-63; callers
+  // treat the queue as broken after a -62 and stop using it).
+  if (Q->broken || hsa_queue_load_read_index_scacquire(q) != hsa_queue_load_write_index_relaxed(q)) return -63;
   const uint64_t n = (uint64_t)r.n;
   const uint64_t base = hsa_queue_add_write_index_relaxed(q, n);
-  // the previous call waited for its last packet, so the queue is empty: this never spins
-  while (base + n - hsa_queue_load_read_index_scacquire(q) > q->size) {
-  }
   hsa_signal_store_relaxed(Q->done, 1);
   hsa_kernel_dispatch_packet_t* ring = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address);
   for (int i = 0; i < r.n; ++i) {
@@ -383,7 +394,10 @@ int aql_run(AqlQueue* Q, const LaunchRecord& r) {
   // after 60 s rather than hang the caller
   const double t0 = now_s();
   while (hsa_signal_wait_scacquire(Q->done, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_ACTIVE) >= 1) {
-    if (now_s() - t0 > 60.0) return -62;
+    if (now_s() - t0 > 60.0) {
+      Q->broken = true;  // packets may still run: nothing of this queue may be reused
+      return -62;
+    }
   }
   return 0;
 }

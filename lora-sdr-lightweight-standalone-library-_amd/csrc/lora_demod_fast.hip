@@ -179,7 +179,7 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, TWP tw) {
 #pragma unroll
     for (int b = 0; b < R; b += 2) {
       if (UNIT)
-        bfly2_unit(x[b], x[b + 1]);
+        bfly2_unit<FMA>(x[b], x[b + 1]);
       else
         bfly2<FMA>(x[b], x[b + 1], tw[k * fs]);
     }
@@ -194,7 +194,7 @@ __device__ __forceinline__ void pass_regs(cf* x, int k, TWP tw) {
       for (int uu = 0; uu < S; ++uu) {
         const int kk = k + MA * uu;
         if (UNIT && uu == 0)
-          bfly4_unit(x[blk], x[blk + S], x[blk + 2 * S], x[blk + 3 * S]);
+          bfly4_unit<FMA>(x[blk], x[blk + S], x[blk + 2 * S], x[blk + 3 * S]);
         else
           bfly4<FMA>(x[blk + uu], x[blk + uu + S], x[blk + uu + 2 * S], x[blk + uu + 3 * S], tw[kk * fs],
                 tw[2 * kk * fs], tw[3 * kk * fs]);
@@ -438,27 +438,7 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
     // sine/cosine on its fractional revolution (v_fract, v_sin_f32, v_cos_f32) instead of
     // glibc's sincosf - not bit-exact (include/lora_mi355x.h states the tolerance).
     constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
-    if constexpr (FMA) {
-      // Certified speculative demod: the lane's points i = l + T*q are T apart, so the
-      // factor of point q is e^{i(ph_l + q*rate*T)}: one hardware sin/cos pair for the
-      // lane's first point, one for the step rate*T (exact in fp32: T is a power of two),
-      // then a fused complex product per point.  Each factor stays within
-      // 4 eps rmax L + 5.4e-6 of the exact one (k_est_fast<SPEC = 2> states the bound and
-      // certifies against the exact reference with it).
-      const float ph0 = start + rate * (float)l;
-      const float rev0 = __builtin_amdgcn_fractf(ph0 * INV_2PI);
-      const float revd = __builtin_amdgcn_fractf((rate * (float)T) * INV_2PI);
-      cf r{__builtin_amdgcn_cosf(rev0), __builtin_amdgcn_sinf(rev0)};
-      const cf wd{__builtin_amdgcn_cosf(revd), __builtin_amdgcn_sinf(revd)};
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        cf v = cmul_t<true>(in[q], r);
-        if (q + 1 < P) r = cmul_t<true>(r, wd);
-        if (hann) v = cscale(v, win[l + T * q]);
-        z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
-      }
-      return;
-    }
+    static_assert(!FMA, "the certified demod rotates with spec_rotate_place");
 #pragma unroll
     for (int q = 0; q < P; ++q) {
       const float ph = start + rate * (float)(l + T * q);
@@ -507,6 +487,41 @@ __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, f
       if (hann) v = cscale(v, win[l + T * q]);
       z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
     }
+  }
+}
+
+// The certified speculative demod's rotation (LoRaDemod.cpp:151-157 up to one constant
+// factor per symbol).  The reference rotates point i of symbol s by e^{i (c + rate i)} with
+// c = rate (s N + t_off): the factor e^{i c} is common to the symbol's points, so it
+// multiplies every bin by one unit-modulus number and changes no |X| - the speculative
+// transform leaves it out and rotates by e^{i rate i} alone.  The lane's points i = l + T q
+// are T apart: factor q is r0 wd^q with r0 = e^{i rate l} and wd = e^{i rate T} (rate T is
+// exact: T is a power of two), each from one hardware sin/cos pair of its fractional
+// revolution, then a packed complex-product recurrence.  certify_list bounds the factors'
+// error (e_spec); the phases stay below rmax N, whatever the symbol's position in the frame.
+template <int SF>
+__device__ __forceinline__ void spec_factors(float rate, int l, v2f* F) {
+  constexpr int T = Geo<SF>::T, P = Geo<SF>::P;
+  constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
+  const float rev0 = __builtin_amdgcn_fractf((rate * (float)l) * INV_2PI);
+  const float revd = __builtin_amdgcn_fractf((rate * (float)T) * INV_2PI);
+  const v2f wd = {__builtin_amdgcn_cosf(revd), __builtin_amdgcn_sinf(revd)};
+  F[0] = v2f{__builtin_amdgcn_cosf(rev0), __builtin_amdgcn_sinf(rev0)};
+#pragma unroll
+  for (int q = 1; q < P; ++q) F[q] = pk_cmul(F[q - 1], wd);
+}
+// the window's samples times the factors (and the Hann window, LoRaDemod.cpp:158-160), in
+// pass-1 leaf order
+template <int SF, bool HANN>
+__device__ __forceinline__ void spec_rotate_place(const cf* in, cf* z, const v2f* F, const float* __restrict__ win,
+                                                  int l) {
+  using G = Geo<SF>;
+  constexpr int T = G::T, P = G::P, R1 = G::R1;
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    cf v = unpk(pk_cmul(pk(in[q]), F[q]));
+    if constexpr (HANN) v = cscale(v, win[l + T * q]);
+    z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
   }
 }
 
@@ -1058,8 +1073,8 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     if constexpr (MODE == 0) {
 #pragma unroll
       for (int pp = 0; pp < P / 2; ++pp) {
-        in[2 * pp] = cmul(in[2 * pp], cf{dt[pp].x, dt[pp].y});
-        in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
+        in[2 * pp] = pk_cmul_ref(in[2 * pp], cf{dt[pp].x, dt[pp].y});
+        in[2 * pp + 1] = pk_cmul_ref(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
       }
     }
     float pm = 0.0f;
@@ -1068,9 +1083,12 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
     }
     LORA_STAMP(1, false);
-    const float start = rate * ((float)((uint32_t)s * (uint32_t)N) + (float)toff);
     cf z[P];
-    rotate_place<SF, true, true, true>(in, z, start, rate, HANN, a.win, lr);
+    {
+      v2f F[P];
+      spec_factors<SF>(rate, lr, F);
+      spec_rotate_place<SF, HANN>(in, z, F, a.win, lr);
+    }
     asm volatile("" : "+v"(pm));
     LORA_STAMP(2, false);
     const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true>(z, rows + (size_t)g * rowc, lr, a, nullptr, twl);
@@ -1187,17 +1205,20 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       if constexpr (MODE == 0) {
 #pragma unroll
         for (int pp = 0; pp < P / 2; ++pp) {
-          in[2 * pp] = cmul(in[2 * pp], cf{dt[pp].x, dt[pp].y});
-          in[2 * pp + 1] = cmul(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
+          in[2 * pp] = pk_cmul_ref(in[2 * pp], cf{dt[pp].x, dt[pp].y});
+          in[2 * pp + 1] = pk_cmul_ref(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
         }
       }
       float pm = 0.0f;
 #pragma unroll
       for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
       asm volatile("" : "+v"(pm));
-      const float start = B.rate * ((float)((uint32_t)B.s * (uint32_t)N) + (float)B.toff);
       cf z[P];
-      rotate_place<SF, true, true, true>(in, z, start, B.rate, HANN, a.win, lr);
+      {
+        v2f F[P];
+        spec_factors<SF>(B.rate, lr, F);
+        spec_rotate_place<SF, HANN>(in, z, F, a.win, lr);
+      }
       asm volatile("" : "+v"(pm));
       // the next block's samples, requested once this block's are consumed (their registers
       // are free again)
@@ -1304,6 +1325,12 @@ __device__ __forceinline__ uint32_t exact_symbol(const KArgs& a, const cf* __res
   return key_index(key);
 }
 
+// Largest error of the hardware sine / cosine the speculative rotation uses: v_sin_f32 /
+// v_cos_f32 of every fp32 x in [0, 1) lie within 1.2541e-7 of sin / cos(2 pi x) (measured
+// exhaustively by tools/micro/hw_sincos_err.hip, re-checked on every GPU test run by
+// test_gpu_dropin); the bound carries 2e-7 (60 % headroom).
+constexpr double kHwSinCosErr = 2.0e-7;
+
 // The certification of a frame's speculative symbols (k_est_fast<SPEC = 2>, k_cert_split):
 // q the frame's exact offsets, LANES lanes per frame (li < LANES this lane's index), the
 // certified sync word written, the rejected symbols listed for k_spec_fix.  Derivation of
@@ -1314,18 +1341,21 @@ __device__ __forceinline__ void certify_list(const KArgs& a, int64_t f, const Fr
   const FrameParams qs = a.fp_spec[f];
   const int per = a.total - 2;
   const bool same_t = qs.t_off == q.t_off;
+  constexpr int T = N >= 16 ? N / 16 : 1;
   const double u = 1.0 / 16777216.0;
   const double E = (8.0 * SF + 42.0) * u;
   const double drate = fabs((double)q.rate - (double)qs.rate);
   const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
   const double tabs = (double)abs(q.t_off);
+  // the speculative rotation factors' error (spec_factors): 33 u rmax T + 16 (fract's
+  // rounding 2 pi 2^-25 + sqrt2 kHwSinCosErr) + 15 (2 sqrt2 u) + the keys' truncation 2^-20
+  const double e_spec = 33.0 * u * rmax * T + 16.0 * (1.87e-7 + 1.4143 * kHwSinCosErr) + 2.6e-6 + 9.6e-7;
   // symbol s certified: its margin d exceeds 4 B (n1 = 2 N x the window's max(|I|,|Q|))
   auto certified = [&](double d, double wmax, int s) {
     const double n1 = 2.0 * N * wmax;
     const double L = (double)(s + 1) * N + tabs;
-    const double e_ref = 3.0 * u * rmax * L + u * rmax * N;
-    const double e_spec = 5.0 * u * rmax * L + u * rmax * N + 8e-6;
-    const double B = n1 * (drate * L + e_ref + e_spec + 2.0 * E);
+    const double e_ref = u * rmax * (L + 2.0 * N);
+    const double B = n1 * (drate * N + e_ref + e_spec + 2.0 * E);
     return same_t && d > 4.0 * B + 0x1p-60;
   };
   const uint2* __restrict__ mg = reinterpret_cast<const uint2*>(a.spec_marg) + f * a.total;
@@ -1685,32 +1715,33 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     // ---- certification of the data symbols the demod computed speculatively ----
     // The demod used the pre-pass offsets qs (rate r', t_off) on the unscaled samples y;
     // the reference uses q (rate r, the same t_off, else the symbol is recomputed) on
-    // fl(y * scale).  Argmax ignores the positive factor `scale`, so compare the
-    // reference's spectrum with scale x the demod's, bin by bin, for data symbol s = 2 + j
-    // (window of N points i, phase argument A + i with A = s N + t_off):
-    //  * the reference's phase fl(fl(r fl(A)) + fl(r i)) is within u (rmax L) of
-    //    r (A + i) for each of its three roundings (A, the product, the sum; L = (s + 1) N
-    //    + |t_off| >= |A + i|) plus u rmax N for fl(r i): e_ref = 3 u rmax L + u rmax N;
-    //  * the demod's factor of point i = l + T q is the hardware sin/cos of
-    //    fract(fl(ph0 fl(1/2pi))) for the lane's first point (ph0 rounded like the
-    //    reference's phase: 3 u rmax L + u rmax N; the product by fl(1/2pi): 2 u rmax L;
-    //    v_sin/v_cos_f32 within 1.26e-7 of sin/cos(2 pi x) for every fp32 x in [0, 1),
-    //    measured exhaustively by tools/micro/hw_sincos_err.hip), then 15 steps of a fused
-    //    complex product by the step factor w = e^{i r' T} (hardware sin/cos of
-    //    fract(fl(fl(r' T) fl(1/2pi))), T a power of two: within 2 u rmax T + 1.8e-7 of
-    //    e^{i r' T}, and each product rounds by <= 2 sqrt2 u): e_spec = 5 u rmax L +
-    //    u rmax N + 2 sqrt2 1.26e-7 + 15 (2 u rmax T + 1.8e-7 + 2 sqrt2 u) < 5 u rmax L +
-    //    u rmax N + 6e-6; the demod ranks bins by keys that truncate |X|^2 by < 16 ulp
-    //    (spec_key), moving |X| by < 2^-20 |X|: e_spec = 5 u rmax L + u rmax N + 8e-6;
-    //  * the two exact phases differ by |r - r'| L;
+    // fl(y * scale).  Argmax ignores the positive factor `scale` and any unit-modulus
+    // factor common to the symbol's points, so compare, bin by bin, the reference's
+    // spectrum with scale x the demod's for symbol s (window of N points i; A = s N + t_off,
+    // L = (s + 1) N + |t_off| >= |A + i|):
+    //  * the reference's phase is fl(c + fl(r i)) with c = fl(r fl(A)) the same for every
+    //    point of the symbol: e^{i c} is a common factor, and what varies with i is r i up
+    //    to the rounding of fl(r i) (u rmax N) and of the sum (u (|c| + rmax N) <= u rmax
+    //    (L + N)): e_ref = u rmax (L + 2 N);
+    //  * the demod rotates by e^{i r' i} alone (spec_factors): r0 = e^{i r' l} from
+    //    fl(r' l) (u rmax T), its product by fl(1/2pi) (2 u rmax T), v_fract_f32's rounding
+    //    of a negative argument (2^-25 revolutions = 1.87e-7) and v_sin/v_cos_f32
+    //    (kHwSinCosErr per component); wd = e^{i r' T} the same without the first term; then
+    //    15 packed products by wd, each rounding by <= 2 sqrt2 u: every factor lies within
+    //    e_spec = 33 u rmax T + 16 (1.87e-7 + sqrt2 kHwSinCosErr) + 15 (2 sqrt2 u) of
+    //    e^{i r' i}; the demod ranks bins by keys that truncate |X|^2 by < 16 ulp (spec_key),
+    //    moving |X| by < 2^-20 |X|, which e_spec adds;
+    //  * the two exact phases r i and r' i differ by at most |r - r'| N;
     //  * every other rounding (the product y * scale, the rotation product, log2 N
-    //    butterfly stages with table twiddles, a Hann window's product (|w| <= 1), |X|^2, the
-    //    demod's v_sqrt_f32 of it - within 1 ulp - and the margin's subtraction) moves a bin
-    //    by at most E sum_i |y_i| per path, E = (8 log2 N + 42) u (a stage's rounding is bounded by its partial sums <=
-    //    sum_i |y_i|); v_sqrt_f32 may flush a denormal argument to 0, an absolute error
-    //    below 2^-63 that the absolute term 2^-60 of the test covers.
+    //    butterfly levels with table twiddles - the packed butterflies of the certified path
+    //    round each output component by <= 6 u (|f0| + .. + |f3|) per radix-4 stage, within
+    //    8 u per level (bfly4) - a Hann window's product (|w| <= 1), |X|^2, the demod's
+    //    v_sqrt_f32 of it - within 1 ulp - and the margin's subtraction) moves a bin by at most
+    //    E sum_i |y_i| per path, E = (8 log2 N + 42) u (a stage's rounding is bounded by its
+    //    partial sums <= sum_i |y_i|); v_sqrt_f32 may flush a denormal argument to 0, an
+    //    absolute error below 2^-63 that the absolute term 2^-60 of the test covers.
     // With n1 = 2 N max(|re|, |im|) over the window >= sum_i |y_i|, each bin moves by less
-    // than B = n1 (|r - r'| L + e_ref + e_spec + 2 E) between the paths, so a speculative
+    // than B = n1 (|r - r'| N + e_ref + e_spec + 2 E) between the paths, so a speculative
     // top bin ahead of the runner-up by d > 2 B is the reference's argmax, strictly (no
     // tie to break).  The kernel requires d > 4 B + 2^-60; a symbol that fails is listed and
     // recomputed exactly with the reference's arithmetic by k_spec_fix, the pipeline's

@@ -32,13 +32,79 @@ struct FrameParams {
 __device__ __forceinline__ cf cmul(cf a, cf b) {
   return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
-// FMA = true: the same product with two fused multiply-adds (fewer roundings, not the
-// reference's arithmetic): only for the speculative demod, whose symbols are certified
-// against a rounding bound (lora_demod_fast.hip, k_est_fast<SPEC = 2>).
+// ---- packed fp32 complex arithmetic (v_pk_*_f32: both components in one instruction) ----
+// A complex value is a VGPR pair (re, im); op_sel / op_sel_hi pick which half of each source
+// feeds the low / high lane and neg_lo / neg_hi negate it, so swaps and the j-rotations of
+// the butterflies cost nothing.  A packed instruction issues at about 0.58 of the scalar
+// fp32 rate while doing two operations (tools/micro/valu_rate.hip).  Every operation is
+// one IEEE fp32 operation (an fma rounds once), so pk_cmul_ref below is bit-identical to
+// cmul; the others are used only by the certified speculative demod, whose rounding bound
+// covers them (lora_demod_fast.hip, certify_list).
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f pk(cf a) { return __builtin_bit_cast(v2f, a); }
+__device__ __forceinline__ cf unpk(v2f a) { return __builtin_bit_cast(cf, a); }
+// a * w with the reference's roundings: (fl(ar wr) - fl(ai wi), fl(ai wr) + fl(ar wi)) = cmul
+__device__ __forceinline__ cf pk_cmul_ref(cf a, cf w) {
+  v2f p, q, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(p) : "v"(pk(a)), "v"(pk(w)));          // (ar wr, ai wr)
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1]" : "=v"(q) : "v"(pk(a)), "v"(pk(w)));             // (ar wi, ai wi)
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(p), "v"(q));
+  return unpk(r);
+}
+// a * w: (fma(-ai, wi, fl(ar wr)), fma(ar, wi, fl(ai wr)))
+__device__ __forceinline__ v2f pk_cmul(v2f a, v2f w) {
+  v2f t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(w));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
+}
+// c + a * w: (fma(-ai, wi, fma(ar, wr, cr)), fma(ar, wi, fma(ai, wr, ci)))
+__device__ __forceinline__ v2f pk_cfma(v2f a, v2f w, v2f c) {
+  v2f t, r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(a), "v"(w), "v"(c));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
+}
+__device__ __forceinline__ v2f pk_add(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ v2f pk_sub(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// a - j b = (ar + bi, ai - br) and a + j b = (ar - bi, ai + br)
+__device__ __forceinline__ v2f pk_sub_j(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ v2f pk_add_j(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// 2 a - b and b - 2 a (one fma per component)
+__device__ __forceinline__ v2f pk_twice_minus(v2f a, v2f b) {
+  v2f r;
+  asm("v_pk_fma_f32 %0, %1, 2.0, %2 op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ v2f pk_minus_twice(v2f b, v2f a) {
+  v2f r;
+  asm("v_pk_fma_f32 %0, %1, -2.0, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// FMA = true: the product with fused multiply-adds (fewer roundings, not the reference's
+// arithmetic), packed: only for the speculative demod, whose symbols are certified against
+// a rounding bound (lora_demod_fast.hip, certify_list).
 template <bool FMA>
 __device__ __forceinline__ cf cmul_t(cf a, cf b) {
   if constexpr (FMA)
-    return {__builtin_fmaf(a.re, b.re, -(a.im * b.im)), __builtin_fmaf(a.re, b.im, a.im * b.re)};
+    return unpk(pk_cmul(pk(a), pk(b)));
   else
     return cmul(a, b);
 }
@@ -47,8 +113,26 @@ __device__ __forceinline__ cf csub(cf a, cf b) { return {a.re - b.re, a.im - b.i
 __device__ __forceinline__ cf cscale(cf a, float s) { return {a.re * s, a.im * s}; }
 
 // kissfft.hh:164-185 kf_bfly4 (forward) on F[0], F[m], F[2m], F[3m].
+// FMA (certified path): the same outputs from twelve packed operations -
+//   A = f0 + w2 f2, B = 2 f0 - A (= f0 - w2 f2), P = w3 f3, C = P + w1 f1, D = C - 2 P
+//   (= w1 f1 - w3 f3); f0 = A + C, f2 = A - C, f1 = B - j D, f3 = B + j D
+// (kissfft's 3 products and 8 sums: 28 scalar operations).  Per component the rounding
+// error of an output is at most 6 u (|f0| + |f1| + |f2| + |f3|) (D's error is C's minus twice
+// P's plus one rounding: 5 u (|f1| + |f3|)), within the bound's 8 u per radix-2 level.
 template <bool FMA = false>
 __device__ __forceinline__ void bfly4(cf& f0, cf& f1, cf& f2, cf& f3, cf w1, cf w2, cf w3) {
+  if constexpr (FMA) {
+    const v2f A = pk_cfma(pk(f2), pk(w2), pk(f0));
+    const v2f B = pk_twice_minus(pk(f0), A);
+    const v2f P = pk_cmul(pk(f3), pk(w3));
+    const v2f C = pk_cfma(pk(f1), pk(w1), P);
+    const v2f D = pk_minus_twice(C, P);
+    f0 = unpk(pk_add(A, C));
+    f2 = unpk(pk_sub(A, C));
+    f1 = unpk(pk_sub_j(B, D));
+    f3 = unpk(pk_add_j(B, D));
+    return;
+  }
   const cf s0 = cmul_t<FMA>(f1, w1);
   const cf s1 = cmul_t<FMA>(f2, w2);
   const cf s2 = cmul_t<FMA>(f3, w3);
@@ -64,8 +148,19 @@ __device__ __forceinline__ void bfly4(cf& f0, cf& f1, cf& f2, cf& f3, cf w1, cf 
 }
 
 // bfly4 with w1 = w2 = w3 = (1, 0), the multiplies skipped: identical outputs up to
-// the sign of zero components (argmax-only callers, see pass_regs).
+// the sign of zero components (argmax-only callers, see pass_regs).  PK: the same sums as
+// packed adds (bit-identical; the certified path's transforms use it).
+template <bool PK = false>
 __device__ __forceinline__ void bfly4_unit(cf& f0, cf& f1, cf& f2, cf& f3) {
+  if constexpr (PK) {
+    const v2f s5 = pk_sub(pk(f0), pk(f2)), a0 = pk_add(pk(f0), pk(f2));
+    const v2f s3 = pk_add(pk(f1), pk(f3)), s4 = pk_sub(pk(f1), pk(f3));
+    f2 = unpk(pk_sub(a0, s3));
+    f0 = unpk(pk_add(a0, s3));
+    f1 = unpk(pk_sub_j(s5, s4));  // s5 + (s4.im, -s4.re)
+    f3 = unpk(pk_add_j(s5, s4));
+    return;
+  }
   const cf s5 = csub(f0, f2);
   const cf a0 = cadd(f0, f2);
   const cf s3 = cadd(f1, f3);
@@ -78,7 +173,14 @@ __device__ __forceinline__ void bfly4_unit(cf& f0, cf& f1, cf& f2, cf& f3) {
 }
 
 // bfly2 with w = (1, 0), the multiply skipped (argmax-only callers, see bfly4_unit).
+template <bool PK = false>
 __device__ __forceinline__ void bfly2_unit(cf& f0, cf& f1) {
+  if constexpr (PK) {
+    const v2f a = pk(f0), t = pk(f1);
+    f1 = unpk(pk_sub(a, t));
+    f0 = unpk(pk_add(a, t));
+    return;
+  }
   const cf a = f0, t = f1;
   f1 = csub(a, t);
   f0 = cadd(a, t);
@@ -87,6 +189,12 @@ __device__ __forceinline__ void bfly2_unit(cf& f0, cf& f1) {
 // kissfft.hh:155-162 kf_bfly2 (forward).
 template <bool FMA = false>
 __device__ __forceinline__ void bfly2(cf& f0, cf& f1, cf w) {
+  if constexpr (FMA) {  // A = f0 + w f1, B = 2 f0 - A: 3 packed operations
+    const v2f A = pk_cfma(pk(f1), pk(w), pk(f0));
+    f1 = unpk(pk_twice_minus(pk(f0), A));
+    f0 = unpk(A);
+    return;
+  }
   const cf t = cmul_t<FMA>(f1, w);
   const cf a = f0;
   f1 = csub(a, t);

@@ -185,8 +185,10 @@ inline void launch(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStream
 // rings the doorbell once and waits for the last packet's completion signal.  Kernel
 // objects are found once per kernel in the code object the HIP runtime loaded
 // (hipKernelNameRefByPtr + the HSA loader extension) and cached.  Return 0 or a negative
-// code naming the step that failed (aql_create: -101 .. -110; aql_run: -22 an unusable
-// record, -120 a kernel object not found, -121 an unexpected kernarg layout, -62 timeout).
+// code naming the step that failed (aql_create: -101 .. -110, -111 the library's code objects are compressed bundles; aql_run, before any packet is
+// written: -22 an unusable record, -120 a kernel object not found, -121 an unexpected kernarg
+// layout, -63 the queue is not idle or broken; after dispatch: -62 timeout, after which the
+// queue is broken - its packets may still run - and aql_destroy leaves it alone).
 struct AqlQueue;
 int aql_create(int device, AqlQueue** out);
 int aql_run(AqlQueue* q, const LaunchRecord& r);

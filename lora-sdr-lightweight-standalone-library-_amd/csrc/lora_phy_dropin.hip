@@ -209,7 +209,21 @@ bool run_frame(lora_phy::detail::device_state& g, const std::complex<float>* sam
   if (nsym < 0) return false;
   if (g.aql && use_aql) {
     const int r = run_frame_aql(g, samples, count, out, nsym, d);
-    if (r != -1) return r == 1;
+    if (r == 1) return true;
+    if (r == 0) return false;  // lora_demod_batch itself refused the frame
+    if (r == -62) {
+      // timed out with packets possibly still running: they read the staging and workspace
+      // and write the outputs there, so the queue and both buffers are abandoned (leaked)
+      // and this and later frames take the HIP path on fresh buffers
+      g.aql = nullptr;
+      g.aql_status = -62;
+      g.dev = g.host = nullptr;
+      g.bytes = g.samples = 0;
+      if (!ensure_buffers(g, std::max<size_t>(count, 1))) return false;
+      return run_frame(g, samples, count, out, false);
+    }
+    // -1 (a launch the queue does not take) and every error raised before a packet is
+    // written (-22, -63, -120, -121): the same frame through HIP
   }
   if (count > 0) {
     if (samples != reinterpret_cast<const std::complex<float>*>(host + d.iq))
@@ -252,6 +266,13 @@ int window_code(lora_phy::window_type w) {
 namespace lora_phy {
 
 void detail::release(device_state& g) {
+  // A workspace destroyed after the HIP runtime has been torn down (static storage duration,
+  // destructors at exit) must not call into it: hipGetDevice failing means it is gone.
+  int cur = 0;
+  if ((g.stream || g.aql || g.dev || g.host || g.plan) && hipGetDevice(&cur) != hipSuccess) {
+    g = device_state{};
+    return;
+  }
   if (g.stream) hipStreamSynchronize(static_cast<hipStream_t>(g.stream));
   if (g.aql) lora::aql_destroy(static_cast<lora::AqlQueue*>(g.aql));
   if (g.dev) hipFree(g.dev);
