@@ -160,7 +160,7 @@ def gather_obj(dist, obj, world):
 # Workloads
 # ---------------------------------------------------------------------------------
 
-def make_input(sf, frames, data_syms, seed, device, snr_db=None, sync=None):
+def make_input(sf, frames, data_syms, seed, device, snr_db=None, sync=None, osr=1):
     import numpy as np
     import torch
 
@@ -168,7 +168,7 @@ def make_input(sf, frames, data_syms, seed, device, snr_db=None, sync=None):
 
     g = torch.Generator(device="cpu").manual_seed(seed)
     syms = torch.randint(0, 1 << sf, (frames, data_syms), generator=g, dtype=torch.int32)
-    iq = amd.modulate(syms.to(device), sf, 1, 125000, 1.0, SYNC if sync is None else sync)
+    iq = amd.modulate(syms.to(device), sf, osr, 125000, 1.0, SYNC if sync is None else sync)
     if snr_db is not None:
         # awgn_sweep_gtest.cpp:76-80: sigma = 10^(-SNR/20), sigma/sqrt(2) per component
         sigma = 10.0 ** (-snr_db / 20.0) / np.sqrt(2.0)
@@ -203,16 +203,21 @@ def stage_times(plan, iq, out, steps, device):
 
 
 def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, precision="exact",
-               inputs=None, sync=None, seed_base=20251015, rank=0, window="none"):
+               inputs=None, sync=None, seed_base=20251015, rank=0, window="none", osr=1, spec=True):
     import torch
 
     import lora_phy_amd as amd
 
     N = 1 << sf
     syms, iq = inputs if inputs is not None else make_input(sf, frames, data_syms, seed_base + rank, device,
-                                                            snr_db, sync)
-    plan = amd.DemodPlan(sf, 1, 125000, window, dechirp=True, mode="legacy", device=device,
-                         precision=precision)
+                                                            snr_db, sync, osr)
+    if not spec:  # the three-launch path (frame max, estimate, demod), for comparison lines
+        os.environ["LORA_MI355X_SPEC"] = "0"
+    try:
+        plan = amd.DemodPlan(sf, osr, 125000, window, dechirp=True, mode="legacy", device=device,
+                             precision=precision)
+    finally:
+        os.environ.pop("LORA_MI355X_SPEC", None)
     out = None
     for _ in range(warmup):
         out = plan.run(iq, out)
@@ -250,7 +255,7 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     wall_max, units = all_max_sum(dist, wall, frames * data_syms * steps)
     total_syms = data_syms + 2
     ms_step = wall * 1e3 / steps
-    B_sym = 8 * N + 2
+    B_sym = 8 * N * osr + 2
     got = out.symbols.to(torch.int32).cpu()
     ser = float((got != syms).float().mean())
     # the symbol pass in the speculative pipeline (ranks sharing a device in a rehearsal
@@ -263,13 +268,15 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     # (the speculative pipeline's symbol pass also demodulates the sync symbols: every
     # window of the frame read once, one index written per data symbol)
     spec = "spec" in kernels
-    dom_bytes = {0: frames * total_syms * 8 * N,             # frame max: the whole IQ
-                 1: frames * (2 * 8 * N + 9),                 # estimate: symbols 0/1 + outputs
-                 2: (frames * (total_syms * 8 * N + 2 * data_syms) if spec
-                     else frames * data_syms * B_sym)}[dom]   # demod
+    W = 8 * N * osr  # bytes per symbol window
+    dom_bytes = {0: frames * total_syms * W,                 # frame max: the whole IQ
+                 1: frames * (2 * W + 9),                     # estimate: symbols 0/1 + outputs
+                 2: (frames * (total_syms * W + 2 * data_syms) if spec
+                     # three-launch demod: every osr-th sample of a window is read
+                     else frames * data_syms * (8 * N + 2))}[dom]
     dom_gbs = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9
     return {
-        "sf": sf, "frames": frames, "data_symbols": frames * data_syms, "iq_bytes": iq.numel() * 8,
+        "sf": sf, "osr": osr, "frames": frames, "data_symbols": frames * data_syms, "iq_bytes": iq.numel() * 8,
         "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ser == 0.0, "ser_vs_tx": ser,
         "kernels": kernels, "spec_recomputed_per_step": fixed,
         "msym_s_data": frames * data_syms / (ms_step * 1e-3) / 1e6,
@@ -611,6 +618,26 @@ def main():
                                                           "noiseless, same data symbols per step")
         del rl
         torch.cuda.empty_cache()
+        # oversampled LEGACY frames (osr 2: gr_lora_sdr_interop.cpp:34's capture shape; osr 4):
+        # the speculative pipeline reads each frame once (the window's every sample for the
+        # frame maximum, every osr-th transformed); the three-launch line reads it twice
+        for osr in (2, 4):
+            ro = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank,
+                            osr=osr)
+            line = variant_summary(ro, r7, f"osr {osr}: {osr} x the IQ bytes per symbol, same data symbols")
+            line["symbol_pass_gbs"] = ro["dominant_gbs"]
+            line["symbol_pass_frac"] = ro["dominant_gbs"] / HBM_PEAK_GBS
+            line["step_bytes"] = ro["step_bytes"]
+            if osr == 2:
+                rt = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank,
+                                osr=osr, inputs=(ro["syms"], ro["iq"]), spec=False)
+                line["three_launch"] = {"ms_per_step": rt["ms_per_step"], "stage_ms": rt["stage_ms"],
+                                        "pipeline_frac": rt["pipeline_gbs"] / HBM_PEAK_GBS,
+                                        "symbols_ok": rt["symbols_ok"], "kernels": rt["kernels"]}
+                del rt
+            extra[f"osr{osr}_sf7"] = line
+            del ro
+            torch.cuda.empty_cache()
         extra["mod_sf7"] = run_modulator(7, args.frames, args.data_symbols, device)
     r12 = None
     if not args.no_sf12:

@@ -1019,7 +1019,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     if (e != hipSuccess) rc = set_error(LORA_EIO, "hipMemsetAsync failed");
   }
   // Speculative single-read pipeline (LoRaDemod.cpp:59-192 reordered, results identical;
-  // LEGACY osr-1 frames, either window):
+  // LEGACY frames at osr 1-4, either window):
   //   1. offset estimate on UNSCALED samples (k_est_split / k_est_fast<SPEC=1>), plus the
   //      maximum of the samples outside the data-symbol windows it implies;
   //   2. every symbol with those offsets on unscaled samples (k_spec_demod), which also
@@ -1034,9 +1034,12 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   // precision; the certification holds it to the EXACT reference.  A sync block of
   // k_spec_demod spans 512/N frames (N < 1024): their byte offsets must fit 31 bits.
   const int64_t sync_frames = plan->N < 1024 ? 512 / plan->N : 1;
-  const bool spec_ok = plan->spec && p.mode == LORA_MODE_LEGACY && p.osr == 1 && p.sf >= 6 &&
+  // Oversampled frames (osr 2-4) take it too: the symbol pass reads every sample of each
+  // window (the frame maximum) and transforms every osr-th one; its buffer offsets need the
+  // frame's bytes below 2^31.
+  const bool spec_ok = plan->spec && p.mode == LORA_MODE_LEGACY && p.osr >= 1 && p.osr <= 4 && p.sf >= 6 &&
                        total >= 3 && total - 2 <= lora::kSpecChunks * (plan->N / 16) &&
-                       sync_frames * frame_stride * 8 < (int64_t(1) << 31);
+                       sync_frames * frame_stride * 8 < (int64_t(1) << 31) && frame_len * 8 < (int64_t(1) << 31);
   if (rc == LORA_OK && spec_ok) {
     KArgs as = a;
     as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows

@@ -221,11 +221,10 @@ __device__ __forceinline__ void pass_regs_T(cf* x, int k, const cf* __restrict__
 }
 
 // pass_regs_T with the twiddles in slot pairs (KArgs::twTB2): one 16-byte load per two.
-template <int R, int MA, bool FMA = false>
-__device__ __forceinline__ void pass_regs_T2(cf* x, int k, const cf* __restrict__ twT2) {
+template <int R, int MA>
+__device__ __forceinline__ void load_tw2(cf* w, int k, const cf* __restrict__ twT2) {
   static_assert(R == 4 || R == 16, "radix-4 / radix-16 passes");
   constexpr int NT = R == 16 ? 15 : 3;
-  cf w[NT];
   const float4* __restrict__ p4 = reinterpret_cast<const float4*>(twT2);
 #pragma unroll
   for (int pp = 0; pp < NT / 2; ++pp) {
@@ -234,6 +233,9 @@ __device__ __forceinline__ void pass_regs_T2(cf* x, int k, const cf* __restrict_
     w[2 * pp + 1] = cf{v.z, v.w};
   }
   w[NT - 1] = twT2[(NT / 2) * MA * 2 + k];
+}
+template <int R, bool FMA>
+__device__ __forceinline__ void pass_regs_w(cf* x, const cf* w) {
 #pragma unroll
   for (int blk = 0; blk < R; blk += 4) bfly4<FMA>(x[blk], x[blk + 1], x[blk + 2], x[blk + 3], w[0], w[1], w[2]);
   if constexpr (R == 16) {
@@ -242,6 +244,19 @@ __device__ __forceinline__ void pass_regs_T2(cf* x, int k, const cf* __restrict_
       bfly4<FMA>(x[uu], x[uu + 4], x[uu + 8], x[uu + 12], w[3 + 3 * uu], w[4 + 3 * uu], w[5 + 3 * uu]);
   }
 }
+template <int R, int MA, bool FMA = false>
+__device__ __forceinline__ void pass_regs_T2(cf* x, int k, const cf* __restrict__ twT2) {
+  cf w[R == 16 ? 15 : 3];
+  load_tw2<R, MA>(w, k, twT2);
+  pass_regs_w<R, FMA>(x, w);
+}
+
+// fft_key's hook between pass B's twiddle loads and its LDS reads (the prefetching symbol
+// pass requests the next block's samples there: vmcnt retires in order, so the transform's
+// own loads are all issued before them)
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
 
 // The other lanes' share of one pass: read R points from LDS, run the stages,
 // either write them back or fold them into the argmax key.
@@ -255,7 +270,7 @@ template <int R, int N, int MA, int SF, int T, int P, bool LAST, bool FMA = fals
           bool TSET = false, bool PACK = false>
 __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __restrict__ tw,
                                          uint64_t& key, const cf* __restrict__ twT = nullptr,
-                                         float* second = nullptr) {
+                                         float* second = nullptr, const cf* wpre = nullptr) {
   constexpr int NG = P / R;
 #pragma unroll
   for (int gg = 0; gg < NG; ++gg) {
@@ -265,6 +280,12 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
     const cf* rb = row + lds_slot<SF>(cc * MA * R + k);  // k < MA, MA*u: disjoint bits
 #pragma unroll
     for (int u = 0; u < R; ++u) xs[u] = rb[lds_slot<SF>(MA * u)];
+    if (wpre) {  // the group's twiddles, loaded by the caller (pass_regs_T2's values)
+      if constexpr (R == 4 || R == 16) {
+        pass_regs_w<R, FMA>(xs, wpre + gg * (R == 16 ? 15 : 3));
+        continue;
+      }
+    }
     if constexpr (R == 4 || R == 16) {
       if (TSET || twT) {
         if constexpr (PAIR)
@@ -505,10 +526,14 @@ __device__ __forceinline__ void spec_factors(float rate, int l, v2f* F) {
   constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
   const float rev0 = __builtin_amdgcn_fractf((rate * (float)l) * INV_2PI);
   const float revd = __builtin_amdgcn_fractf((rate * (float)T) * INV_2PI);
-  const v2f wd = {__builtin_amdgcn_cosf(revd), __builtin_amdgcn_sinf(revd)};
+  const float cd = __builtin_amdgcn_cosf(revd), sd = __builtin_amdgcn_sinf(revd);
+  // Written as plain vector arithmetic, not the v_pk_* asm helpers: the hazard recognizer
+  // does not see an asm instruction read a transcendental's result (gfx950 needs a wait
+  // state there), and the loop-invariant (-sd, sd) makes each step two packed operations.
+  const v2f wdr = {cd, cd}, wdi = {-sd, sd};
   F[0] = v2f{__builtin_amdgcn_cosf(rev0), __builtin_amdgcn_sinf(rev0)};
 #pragma unroll
-  for (int q = 1; q < P; ++q) F[q] = pk_cmul(F[q - 1], wd);
+  for (int q = 1; q < P; ++q) F[q] = __builtin_elementwise_fma(F[q - 1].yx, wdi, F[q - 1] * wdr);
 }
 // the window's samples times the factors (and the Hann window, LoRaDemod.cpp:158-160), in
 // pass-1 leaf order
@@ -525,31 +550,47 @@ __device__ __forceinline__ void spec_rotate_place(const cf* in, cf* z, const v2f
   }
 }
 
-// Pass 1's twiddles (MA = 1: indices multiples of N/16, at most 9 N/16) held in registers
-// and indexed like the table (the prefetching speculative demod loads them before its next
-// round's samples, so no vector load follows those inside the transform).
+// Pass 1's twiddles in the certified transforms: indices m N/16 (MA = 1; m <= 9), i.e.
+// e^{-2 pi i m / 16}, as fp32 constants (correctly rounded: the table's values up to its own
+// rounding, which the certification's E carries either way).  Loaded from the table every
+// round they cost the prefetching symbol pass 5 % at SF7 (an L2 round trip per round).
+__device__ __forceinline__ cf w16(int m) {
+  constexpr float C1 = 0.923879532511286756f, S1 = 0.382683432365089772f, R2 = 0.707106781186547524f;
+  switch (m) {
+    case 0: return cf{1.0f, 0.0f};
+    case 1: return cf{C1, -S1};
+    case 2: return cf{R2, -R2};
+    case 3: return cf{S1, -C1};
+    case 4: return cf{0.0f, -1.0f};
+    case 5: return cf{-S1, -C1};
+    case 6: return cf{-R2, -R2};
+    case 7: return cf{-C1, -S1};
+    case 8: return cf{-1.0f, 0.0f};
+    default: return cf{-C1, S1};
+  }
+}
 template <int N>
-struct RegTw1 {
-  cf v[10];
-  __device__ __forceinline__ cf operator[](int i) const { return v[i / (N / 16)]; }
+struct ConstTw1 {
+  __device__ __forceinline__ cf operator[](int i) const { return w16(i / (N / 16)); }
 };
 
 // FFT of the symbol held as pass-1 inputs in z (T lanes x P points) and the lane's
 // argmax key.  KEEP: leave the spectrum in natural order in `row` (padded address
 // paddr(bin)) for the estimate's neighbour bins; NPASS == 1 keeps it in z.
-// CPRE: the pass-1 write-back positions c[h] (rev[l + T h] >> LOGR1) and pass 1's twiddles
-// (tw1) come from the caller instead of vector loads.
-template <int SF, bool KEEP, bool FMA = false, bool TWL = false, bool PACK = false, bool CPRE = false>
+// CPRE: the pass-1 write-back positions c[h] (rev[l + T h] >> LOGR1) come from the caller
+// instead of vector loads.  FMA (the certified transforms): pass 1's twiddles are constants
+// (ConstTw1).
+template <int SF, bool KEEP, bool FMA = false, bool TWL = false, bool PACK = false, bool CPRE = false,
+          class HOOK = NoHook>
 __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr,
-                                            const cf* twl = nullptr, const int* cpre = nullptr,
-                                            const RegTw1<(1 << SF)>* tw1 = nullptr) {
+                                            const cf* twl = nullptr, const int* cpre = nullptr, HOOK hook = HOOK{}) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
   constexpr bool WL = G::WAVE_LOCAL;
 #pragma unroll
   for (int h = 0; h < G::G1; ++h) {
-    if constexpr (CPRE)
-      pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP, FMA, RegTw1<N>>(z + h * R1, 0, *tw1);
+    if constexpr (FMA)
+      pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP, FMA, ConstTw1<N>>(z + h * R1, 0, ConstTw1<N>{});
     else
       pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP, FMA>(z + h * R1, 0, a.tw);
   }
@@ -588,8 +629,20 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
       write_pass<G::RA, G::MA_A, SF, T, P>(row, z, l);
       block_sync<WL>();
       // TWL (speculative demod): pass B's twiddles two per 16-byte load (KArgs::twTB2)
-      pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR, TWL, PACK>(
-          row, z, l, a.tw, key, ((TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
+      if constexpr (!std::is_same_v<HOOK, NoHook>) {
+        // every group's twiddles first, then the hook, then the pass
+        constexpr int NT = G::RB == 16 ? 15 : 3;
+        cf wb[(P / G::RB) * NT];
+#pragma unroll
+        for (int gg = 0; gg < P / G::RB; ++gg) load_tw2<G::RB, G::MA_B>(wb + gg * NT, (l + T * gg) % G::MA_B, a.twTB2);
+        __builtin_amdgcn_sched_barrier(0);
+        hook();
+        __builtin_amdgcn_sched_barrier(0);
+        pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, true, TWL, PACK>(row, z, l, a.tw, key, a.twTB2, second, wb);
+      } else {
+        pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR, TWL, PACK>(
+            row, z, l, a.tw, key, ((TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
+      }
     }
     if constexpr (KEEP) {
       // last-pass outputs: bin = (l + T*gg) + ML*u (cc == 0)
@@ -704,66 +757,74 @@ __device__ __forceinline__ void group_reduce2(float& a, float& b, int tid, float
   }
 }
 
-// Speculative demod: exchange with lane ^ o (o < 64) - DPP for o <= 8 (the values of a
-// reduction step are uniform over each aligned block of o lanes, so a mirror inside the
-// next block up is the same exchange), a lane permute beyond.
-template <int O>
-__device__ __forceinline__ uint32_t xchg_u32(uint32_t v) {
-  if constexpr (O == 1)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  else if constexpr (O == 2)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  else if constexpr (O == 4)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  else if constexpr (O == 8)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
-  else
-    return (uint32_t)__shfl_xor((int)v, O, 64);
-}
-
 // (best, second) of the symbol's bins from every lane's (best, second) keys, and the max
 // of pm, over the symbol's T lanes (every lane gets them): the second is the runner-up of
 // the whole multiset of bins, so two lanes holding equal best keys give a zero margin.
+// pm (a maximum of absolute values: never negative, never NaN) travels as its bits, which
+// order like the values.  The merge of two (best, second, max) triples is symmetric, so an
+// exchange may hand a lane its own values back in either slot: steps 1-8 are DPP movs the
+// compiler folds into the unsigned max / min (aligned blocks hold one value per step, so a
+// mirror inside the next block up is the xor exchange), 16 and 32 the row / half swaps
+// (v_permlane16_swap_b32, v_permlane32_swap_b32: one lane ends with each of the two
+// values of its pair in the two slots).
+__device__ __forceinline__ void top2_merge(uint32_t& b, uint32_t& s, uint32_t& p, uint32_t b2, uint32_t s2,
+                                           uint32_t p2) {
+  const uint32_t lo = b < b2 ? b : b2;
+  const uint32_t hs = s > s2 ? s : s2;
+  s = hs > lo ? hs : lo;
+  b = b > b2 ? b : b2;
+  p = p > p2 ? p : p2;
+}
+template <int O>
+__device__ __forceinline__ uint32_t dpp_xchg(uint32_t v) {
+  constexpr int ctrl = O == 1 ? 0xB1 : O == 2 ? 0x4E : O == 4 ? 0x141 : 0x140;  // quad perms, half / row mirror
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xF, 0xF, true);
+}
 template <int O, int W>
-__device__ __forceinline__ void spec_reduce_step(uint32_t& best, uint32_t& sec, float& pm) {
+__device__ __forceinline__ void spec_reduce_step(uint32_t& best, uint32_t& sec, uint32_t& pm) {
   if constexpr (O < W) {
-    const uint32_t ob = xchg_u32<O>(best), os = xchg_u32<O>(sec);
-    const float op = __uint_as_float(xchg_u32<O>(__float_as_uint(pm)));
-    const uint32_t lo = best < ob ? best : ob;
-    const uint32_t s2 = sec > os ? sec : os;
-    sec = s2 > lo ? s2 : lo;
-    best = best > ob ? best : ob;
-    pm = fmaxf(pm, op);
+    if constexpr (O <= 8) {
+      top2_merge(best, sec, pm, dpp_xchg<O>(best), dpp_xchg<O>(sec), dpp_xchg<O>(pm));
+    } else if constexpr (O == 16) {
+      const auto xb = __builtin_amdgcn_permlane16_swap(best, best, false, false);
+      const auto xs = __builtin_amdgcn_permlane16_swap(sec, sec, false, false);
+      const auto xp = __builtin_amdgcn_permlane16_swap(pm, pm, false, false);
+      best = xb[0], sec = xs[0], pm = xp[0];
+      top2_merge(best, sec, pm, xb[1], xs[1], xp[1]);
+    } else {
+      static_assert(O == 32, "wave64");
+      const auto xb = __builtin_amdgcn_permlane32_swap(best, best, false, false);
+      const auto xs = __builtin_amdgcn_permlane32_swap(sec, sec, false, false);
+      const auto xp = __builtin_amdgcn_permlane32_swap(pm, pm, false, false);
+      best = xb[0], sec = xs[0], pm = xp[0];
+      top2_merge(best, sec, pm, xb[1], xs[1], xp[1]);
+    }
     spec_reduce_step<2 * O, W>(best, sec, pm);
   }
 }
 template <int SF>
-__device__ __forceinline__ void spec_reduce(uint32_t& best, uint32_t& sec, float& pm, int tid, uint32_t* scratch) {
+__device__ __forceinline__ void spec_reduce(uint32_t& best, uint32_t& sec, float& pmf, int tid, uint32_t* scratch) {
   constexpr int T = Geo<SF>::T;
+  uint32_t pm = __float_as_uint(pmf);
   spec_reduce_step<1, (T < 64 ? T : 64)>(best, sec, pm);
   if constexpr (T > 64) {  // waves of one symbol: one LDS round (3 words per wave)
     const int w = tid >> 6;
     if ((tid & 63) == 0) {
       scratch[3 * w] = best;
       scratch[3 * w + 1] = sec;
-      scratch[3 * w + 2] = __float_as_uint(pm);
+      scratch[3 * w + 2] = pm;
     }
     __syncthreads();
     constexpr int WPS = T / 64;
     const int wb = (w / WPS) * WPS;
     best = scratch[3 * wb];
     sec = scratch[3 * wb + 1];
-    pm = __uint_as_float(scratch[3 * wb + 2]);
+    pm = scratch[3 * wb + 2];
 #pragma unroll
-    for (int q = 1; q < WPS; ++q) {
-      const uint32_t ob = scratch[3 * (wb + q)], os = scratch[3 * (wb + q) + 1];
-      const uint32_t lo = best < ob ? best : ob;
-      const uint32_t s2 = sec > os ? sec : os;
-      sec = s2 > lo ? s2 : lo;
-      best = best > ob ? best : ob;
-      pm = fmaxf(pm, __uint_as_float(scratch[3 * (wb + q) + 2]));
-    }
+    for (int q = 1; q < WPS; ++q)
+      top2_merge(best, sec, pm, scratch[3 * (wb + q)], scratch[3 * (wb + q) + 1], scratch[3 * (wb + q) + 2]);
   }
+  pmf = __uint_as_float(pm);
 }
 
 // MODE 0: LEGACY + fused dechirp, osr 1, no window (the benchmark configuration);
@@ -795,6 +856,19 @@ constexpr int demod_twl_entries() {
   }
 }
 
+
+// k_spec_demod's LDS: the symbol rows, pass A's twiddles, then (prefetching geometries) the
+// dechirp table's pairs at table phase 0, 16-byte aligned.
+template <int SF>
+constexpr size_t spec_dtl_offset() {
+  return (((size_t)Geo<SF>::SPW * lds_row<SF>() + demod_twl_entries<SF, true>()) * sizeof(cf) + 15) & ~(size_t)15;
+}
+template <int SF>
+constexpr size_t spec_lds_bytes() {
+  constexpr bool pf2 = Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2;
+  return pf2 ? spec_dtl_offset<SF>() + 16 * 8 * Geo<SF>::T
+             : sizeof(cf) * ((size_t)Geo<SF>::SPW * lds_row<SF>() + demod_twl_entries<SF, true>());
+}
 
 // SPEC: the speculative single-read pipeline's symbol pass (lora_capi.hip): the pre-pass
 // offsets (fp_spec) on unscaled samples, and per data symbol (spec_marg, one 8-byte
@@ -952,7 +1026,11 @@ __device__ __forceinline__ void stamp(int k, bool real) {
 #ifndef LORA_SPEC_RAWSQRT
 #define LORA_SPEC_RAWSQRT 1  // margins from v_sqrt_f32 instead of IEEE sqrtf (-0.5 %)
 #endif
-template <int SF, int MODE, bool HANN = false>
+// OSRN: oversampled frames (LEGACY osr 2-4, a.osr at run time): a symbol's points are every
+// osr-th sample of its window (LoRaDemod.cpp:141-157 reads sym_samps[i * osr]), and the
+// window's other samples are read with them for the frame maximum, which the reference takes
+// over every sample (LoRaDemod.cpp:59-67) - the frame is still read once.
+template <int SF, int MODE, bool HANN = false, bool OSRN = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   using G = Geo<SF>;
@@ -961,7 +1039,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   constexpr int SPB = WL ? 64 / T : SPW;  // symbols per block
   constexpr int BPG = WL ? 4 : 1;         // blocks per workgroup round
   constexpr int NTW = demod_twl_entries<SF, true>();
-  static_assert(P == 16 && (MODE == 0 || MODE == 1), "SF >= 6, LEGACY osr 1");
+  static_assert(P == 16 && (MODE == 0 || MODE == 1), "SF >= 6, LEGACY (osr 1, or OSRN)");
   static_assert(NTW <= 256, "one staged twiddle per thread");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t red3[3 * 4];  // spec_reduce's cross-wave words (T > 64)
@@ -969,9 +1047,17 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   cf* twl = rows + (size_t)SPW * rowc;
   const int tot = a.total;
   const int per = tot - 2;
+  // (PF geometries, MODE 0) the dechirp table's pairs at table phase 0 - what every window
+  // of a t_off = 0 frame reads - staged after the twiddles: dtl[p T + c] = downP[p (N + T) + c]
+  constexpr bool DTL = LORA_SPEC_PF && WL && G::NPASS == 2 && !OSRN && MODE == 0;
+  float4* dtl = reinterpret_cast<float4*>(smem + spec_dtl_offset<SF>());
   if constexpr (NTW > 0) {
     const int tid = threadIdx.x;
     if (tid < NTW) twl[tid] = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
+    if constexpr (DTL) {
+      static_assert(8 * T <= 256, "one staged pair per thread");
+      if (tid < 8 * T) dtl[tid] = reinterpret_cast<const float4*>(a.downP)[(tid / T) * (N + T) + tid % T];
+    }
     __syncthreads();
   }
   const int bpf = (per + SPB - 1) / SPB;  // data blocks per frame
@@ -1017,9 +1103,34 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     const FrameParams fp = a.fp_spec[f];
     const float rate = fp.rate;
     const int toff = fp.t_off;
+    const int step = OSRN ? a.step : N;
     int64_t base;
     int cg;
-    sym_base(s, N, a.frame_len, toff, base, cg);
+    sym_base(s, step, a.frame_len, toff, base, cg);
+    cf in[P];
+    float pm = 0.0f;
+    int lr = l;
+    if constexpr (OSRN) {
+      // point q of lane l is sample base + (l + T q) osr; the osr samples from it on are
+      // dechirped (MODE 0: table down[cg + j], no wrap) and enter the window's maximum
+      const int osr = a.osr;
+      const __amdgpu_buffer_rsrc_t rx =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + fu * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)a.down, (short)0, 0x7fffffff, 0x00020000);
+      const int vo = rel + (int)(base + (int64_t)l * osr) * 8;
+      const int vt = (cg + l * osr) * 8;
+      const int so = T * osr * 8;  // bytes between a lane's points
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        for (int k = 0; k < osr; ++k) {
+          cf y = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, vo + 8 * k, q * so, 2 /* nt */));
+          if constexpr (MODE == 0)
+            y = pk_cmul_ref(y, __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rd, vt + 8 * k, q * so, 0)));
+          if constexpr (!SYNC) pm = amax3(pm, y);
+          if (k == 0) in[q] = y;
+        }
+      }
+    } else {
     // The window's samples (read once: nontemporal) through a buffer resource on the
     // wave-uniform frame base: the point offsets T q (up to 30 KB at SF12) go in the scalar
     // offset or the immediate, not in 64-bit vector adds.  Byte offsets fit 31 bits: the
@@ -1034,7 +1145,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     constexpr int D = T < 8 ? T : 8;
     constexpr bool AL = LORA_SPEC_ALIGN;
     const int d = AL ? (int)(base & (D - 1)) : 0;
-    const int lr = AL ? ((l - d) & (T - 1)) : l;
+    lr = AL ? ((l - d) & (T - 1)) : l;
     v2f ld[P + 1];
     const __amdgpu_buffer_rsrc_t rx =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + fu * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
@@ -1064,7 +1175,6 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
 #pragma unroll
       for (int q = 0; q < P; ++q) ld[q] = late ? ld[q + 1] : ld[q];  // ascending: ld[q + 1] not yet moved
     }
-    cf in[P];
 #pragma unroll
     for (int q = 0; q < P; ++q) in[q] = cf{ld[q].x, ld[q].y};
     // caller-side dechirp (e2e_chain_test.cpp:88-93) with the reference's products, the
@@ -1077,11 +1187,11 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
         in[2 * pp + 1] = pk_cmul_ref(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
       }
     }
-    float pm = 0.0f;
     if constexpr (!SYNC) {
 #pragma unroll
       for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
     }
+    }  // osr 1
     LORA_STAMP(1, false);
     cf z[P];
     {
@@ -1129,7 +1239,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   // loaded with the table pairs ahead of the prefetch, pass A's are in LDS - so no wait on
   // the current block's operands also waits for the next block's samples (vmcnt retires in
   // order).
-  constexpr bool PF = LORA_SPEC_PF && WL && G::NPASS == 2;
+  constexpr bool PF = LORA_SPEC_PF && WL && G::NPASS == 2 && !OSRN;
   if constexpr (PF) {
     constexpr int D = T < 8 ? T : 8;
     const int tid0 = threadIdx.x;
@@ -1186,13 +1296,14 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
         const __amdgpu_buffer_rsrc_t rd =
             __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
         const int vt = (B.cg + lr) * 16;
+        // every window of the wave at table phase 0 (t_off = 0 frames): the LDS slice
+        const bool cg0 = __builtin_amdgcn_readfirstlane(__ballot(B.cg != 0) == 0);
 #pragma unroll
         for (int pp = 0; pp < P / 2; ++pp)
-          dt[pp] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vt, pp * (N + T) * 16, 0));
+          dt[pp] = cg0 ? dtl[pp * T + lr]
+                       : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vt, pp * (N + T) * 16, 0));
       }
-      RegTw1<N> t1;
-#pragma unroll
-      for (int m = 0; m < 10; ++m) t1.v[m] = a.tw[m * (N / 16)];
+
       // select (a misaligned window), dechirp, window max
       if (B.mis) {
         const bool late = l < d;
@@ -1229,8 +1340,8 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       int cpre[G::G1];
 #pragma unroll
       for (int h = 0; h < G::G1; ++h) cpre[h] = __shfl(cown[h], lane0 + lr, 64);
-      const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true, true>(z, rows + (size_t)g * rowc, lr, a, nullptr,
-                                                                           twl, cpre, &t1);
+      const uint64_t lk =
+          fft_key<SF, false, true, (NTW > 0), true, true>(z, rows + (size_t)g * rowc, lr, a, nullptr, twl, cpre);
       const uint32_t lbest = (uint32_t)lk;
       uint32_t best = lbest, sec = (uint32_t)(lk >> 32);
       spec_reduce<SF>(best, sec, pm, tid0, red3);
@@ -1247,6 +1358,123 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
           reinterpret_cast<uint2*>(a.spec_marg)[B.f * tot + B.s] = make_uint2(__float_as_uint(margin), __float_as_uint(pm));
       }
       wave_sync();  // the rows are rewritten by the next round
+    }
+  }
+  // PF3 (three-pass geometries, SF 10-12): the same prefetching loop; the next block's
+  // samples are requested at pass B, after every vector load of the transform (the pass-1
+  // positions and twiddles, pass B's twiddle pairs - all older, so waiting for them never
+  // waits for the prefetch).  SF 11-12: a block is the workgroup's symbol.
+  constexpr bool PF3 = LORA_SPEC_PF && G::NPASS == 3 && !OSRN;
+  if constexpr (PF3) {
+    constexpr int D = T < 8 ? T : 8;
+    const int tid0 = threadIdx.x;
+    const int g = SPW == 1 ? 0 : tid0 / T;
+    const int l = tid0 % T;
+    const int gi = WL ? g % SPB : g;
+    const __attribute__((address_space(4))) FrameParams* fps =
+        (const __attribute__((address_space(4))) FrameParams*)a.fp_spec;
+    struct Blk {
+      int64_t f;
+      int s, d, cg;
+      bool valid, mis;
+      float rate;
+      int toff;
+    };
+    // pass-1 positions of role l (an aligned window's roles are the lanes themselves)
+    int cown[G::G1];
+#pragma unroll
+    for (int h = 0; h < G::G1; ++h) cown[h] = (int)(a.rev[l + T * h] >> G::LOGR1);
+    v2f nx[P + 1];
+    auto issue = [&](int64_t bb, Blk& B) {
+      B.f = bb / bpf;
+      const int jl = (int)(bb - B.f * bpf) * SPB + gi;
+      B.valid = jl < per;
+      B.s = 2 + (B.valid ? jl : per - 1);
+      B.rate = fps[B.f].rate;
+      B.toff = fps[B.f].t_off;
+      int64_t base;
+      sym_base(B.s, N, a.frame_len, B.toff, base, B.cg);
+      B.d = (int)(base & (D - 1));
+      B.mis = __builtin_amdgcn_readfirstlane(__ballot(l < B.d) != 0);  // waves holding late lanes
+      const __amdgpu_buffer_rsrc_t rx =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + B.f * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
+      const int vo = (int)(base - B.d + l) * 8;
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+        nx[q] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
+      if (B.mis)
+        nx[P] = __builtin_bit_cast(
+            v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, l < B.d ? vo : vo - T * 8, P * T * 8, 2 /* nt */));
+    };
+    int64_t b = grp0 * BPG + (WL ? wave : 0);
+    Blk nb{};
+    if (b < dblocks) issue(b, nb);
+    for (; b < dblocks; b += gstride * BPG, grp0 += gstride) {
+      const Blk B = nb;
+      v2f(&ld)[P + 1] = nx;
+      const int d = B.d;
+      const int lr = (l - d) & (T - 1);
+      float4 dt[MODE == 0 ? P / 2 : 1];
+      if constexpr (MODE == 0) {
+        const __amdgpu_buffer_rsrc_t rd =
+            __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
+        const int vt = (B.cg + lr) * 16;
+#pragma unroll
+        for (int pp = 0; pp < P / 2; ++pp)
+          dt[pp] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vt, pp * (N + T) * 16, 0));
+      }
+      if (B.mis) {
+        const bool late = l < d;
+#pragma unroll
+        for (int q = 0; q < P; ++q) ld[q] = late ? ld[q + 1] : ld[q];
+      }
+      cf in[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) in[q] = cf{ld[q].x, ld[q].y};
+      if constexpr (MODE == 0) {
+#pragma unroll
+        for (int pp = 0; pp < P / 2; ++pp) {
+          in[2 * pp] = pk_cmul_ref(in[2 * pp], cf{dt[pp].x, dt[pp].y});
+          in[2 * pp + 1] = pk_cmul_ref(in[2 * pp + 1], cf{dt[pp].z, dt[pp].w});
+        }
+      }
+      float pm = 0.0f;
+#pragma unroll
+      for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
+      asm volatile("" : "+v"(pm));
+      cf z[P];
+      {
+        v2f F[P];
+        spec_factors<SF>(B.rate, lr, F);
+        spec_rotate_place<SF, HANN>(in, z, F, a.win, lr);
+      }
+      asm volatile("" : "+v"(pm));
+      const int64_t bn = b + gstride * BPG;
+      auto hook = [&]() {
+        if (bn < dblocks) issue(bn, nb);
+      };
+      // role lr's pass-1 positions: the lane's own for an aligned window, else a table load
+      // (issued before the prefetch, so waiting for it never waits for the next samples)
+      int cpre[G::G1];
+#pragma unroll
+      for (int h = 0; h < G::G1; ++h) cpre[h] = d == 0 ? cown[h] : (int)(a.rev[lr + T * h] >> G::LOGR1);
+      const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true, true, decltype(hook)>(
+          z, rows + (size_t)g * rowc, lr, a, nullptr, twl, cpre, hook);
+      const uint32_t lbest = (uint32_t)lk;
+      uint32_t best = lbest, sec = (uint32_t)(lk >> 32);
+      spec_reduce<SF>(best, sec, pm, tid0, red3);
+      if (B.valid) {
+        constexpr int NG = P / G::RB;
+        constexpr int ML = G::MA_B;
+        const int o = (int)(best & 15u);
+        const uint32_t idx = (uint32_t)(lr + T * (o % NG) + ML * (o / NG));
+        const float margin =
+            __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec));
+        if (lbest == best && a.syms) a.syms[B.f * a.sym_stride + (B.s - 2)] = (uint16_t)idx;
+        if (l == 0)
+          reinterpret_cast<uint2*>(a.spec_marg)[B.f * tot + B.s] = make_uint2(__float_as_uint(margin), __float_as_uint(pm));
+      }
+      block_sync<WL>();  // the rows (and red3) are rewritten by the next round
     }
   }
   // (an incremental quotient / remainder instead of the 64-bit division per round measured
@@ -1425,7 +1653,8 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   constexpr int N = G::N, T = G::T, P = G::P;
   constexpr int SPB = (T >= 64 ? 256 : 64) / T;  // frames per block (block = max(T, 64))
   constexpr bool DYN = MODE == 2;
-  static_assert(SPEC == 0 || !DYN, "the speculative pipeline covers MODE 0/1 only");
+  // (the speculative pipeline's stages run MODE 0/1 at osr 1 and MODE 2 for oversampled
+  // LEGACY frames)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint64_t red[4];
   __shared__ FrameParams sp[SPB];
@@ -2171,32 +2400,38 @@ int device_cus() {
   return cache[dev];
 }
 
-template <int SF, int MODE, bool HANN>
+template <int SF, int MODE, bool HANN, bool OSRN>
 bool launch_spec_demod_w(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
-  const size_t lds = sizeof(cf) * ((size_t)G::SPW * rowc + demod_twl_entries<SF, true>());
+  const size_t lds = spec_lds_bytes<SF>();
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN, OSRN>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return false;
   // the kernel's blocks: SPB symbols of one frame (see k_spec_demod), BPG per workgroup round
   constexpr int SPB = G::WAVE_LOCAL ? 64 / G::T : G::SPW, BPG = G::WAVE_LOCAL ? 4 : 1;
   const int per = a.total - 2;
   const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB) + (2 * frames + SPB - 1) / SPB;
   const int64_t groups = (blocks + BPG - 1) / BPG;
-  const bool persist = LORA_SPEC_PERSIST == 2 || (LORA_SPEC_PERSIST == 1 && G::WAVE_LOCAL);
+  // persistent: the wave-local geometries, and every prefetching one (PF3: SF 10-12)
+  const bool persist = LORA_SPEC_PERSIST == 2 || (LORA_SPEC_PERSIST == 1 && G::WAVE_LOCAL) ||
+                       (LORA_SPEC_PF && G::NPASS == 3 && a.osr == 1);
   const int64_t cap = persist ? (int64_t)device_cus() * LORA_SPEC_WG_PER_CU : groups;
   const int64_t grid = groups < cap ? groups : cap;
-  launch(k_spec_demod<SF, MODE, HANN>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
+  launch(k_spec_demod<SF, MODE, HANN, OSRN>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
   return true;
 }
-// the Hann window (LoRaDemod.cpp:158-160) as an instantiation of its own: the unwindowed
-// kernels keep no per-point branch
+// the Hann window (LoRaDemod.cpp:158-160) and oversampling as instantiations of their own:
+// the unwindowed osr-1 kernels keep no per-point branch
 template <int SF, int MODE>
 bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
-  return a.hann ? launch_spec_demod_w<SF, MODE, true>(a, frames, st) : launch_spec_demod_w<SF, MODE, false>(a, frames, st);
+  if (a.osr > 1)
+    return a.hann ? launch_spec_demod_w<SF, MODE, true, true>(a, frames, st)
+                  : launch_spec_demod_w<SF, MODE, false, true>(a, frames, st);
+  return a.hann ? launch_spec_demod_w<SF, MODE, true, false>(a, frames, st)
+                : launch_spec_demod_w<SF, MODE, false, false>(a, frames, st);
 }
 
 // k_spec_fix's grid: one workgroup per CU (or fewer when the frames hold fewer data
@@ -2224,6 +2459,13 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   if constexpr (SF < 6) {
     return false;
   } else {
+    if (a.osr > 1) {  // oversampled frames: the estimate stages at run-time osr (MODE 2)
+      if (stage == 0) return launch_est_mode<SF, 2, 1>(a, frames, st);
+      if (stage == 1)
+        return a.dechirp ? launch_spec_demod<SF, 0>(a, frames, st) : launch_spec_demod<SF, 1>(a, frames, st);
+      if (stage == 2) return launch_est_mode<SF, 2, 2>(a, frames, st);
+      return launch_spec_fix<SF, 2>(a, frames, st);
+    }
     if constexpr (SF <= 9 && LORA_EST_SPLIT) {
       if (stage == 0) return a.dechirp ? launch_est_split<SF, 0>(a, frames, st) : launch_est_split<SF, 1>(a, frames, st);
       if (stage == 2 && LORA_CERT_SPLIT)

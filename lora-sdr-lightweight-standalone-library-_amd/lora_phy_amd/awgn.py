@@ -131,8 +131,12 @@ def simulate(sf: int, cr: str, snr_db: float, packets: int, payload_len: int, up
 
 def sweep_chain(sf: int, snr_dbs: Sequence[float], frames: int = 1000, payload_len: int = 16,
                 seed: int = 1234, cfo_bins: float = 0.0, osr: int = 1, device=None,
-                keep_iq: bool = False) -> List[Dict]:
-    """SER / BER / PER of encode -> modulate -> AWGN (+CFO) -> LEGACY demod -> decode."""
+                keep_iq: bool = False, exact_check: bool = False) -> List[Dict]:
+    """SER / BER / PER of encode -> modulate -> AWGN (+CFO) -> LEGACY demod -> decode.
+
+    exact_check: also run every point through the three-launch exact path (the oracle-pinned
+    kernels, LORA_MI355X_SPEC=0) and count the frames whose symbols, sync word or cfo /
+    time_offset bits differ from the default (speculative, certified) pipeline's."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     N = 1 << sf
     rng = np.random.default_rng(seed)
@@ -145,12 +149,22 @@ def sweep_chain(sf: int, snr_dbs: Sequence[float], frames: int = 1000, payload_l
         ph = 2.0 * math.pi * cfo_bins * nn / (N * osr)
         clean = (clean.to(torch.complex128) * torch.polar(torch.ones_like(ph), ph)).to(torch.complex64)
     plan = DemodPlan(sf, osr, 125000, "none", dechirp=True, mode="legacy", device=dev)
+    xplan = None
+    if exact_check:
+        import os
+
+        os.environ["LORA_MI355X_SPEC"] = "0"
+        try:
+            xplan = DemodPlan(sf, osr, 125000, "none", dechirp=True, mode="legacy", device=dev)
+        finally:
+            os.environ.pop("LORA_MI355X_SPEC", None)
     gen = torch.Generator(device=dev).manual_seed(seed + 1)
     out = []
     for snr in snr_dbs:
         sigma = 10.0 ** (-snr / 20.0) / math.sqrt(2.0)
         noise = torch.randn((frames, L, 2), generator=gen, device=dev) * sigma
         iq = clean + torch.view_as_complex(noise)
+        fixed0 = plan.spec_recomputed()
         res = plan.run(iq)
         rx = res.symbols.to(torch.int64).cpu().numpy()
         dec = codes.lora_decode(rx)
@@ -160,7 +174,15 @@ def sweep_chain(sf: int, snr_dbs: Sequence[float], frames: int = 1000, payload_l
         diff = np.bitwise_xor(dec, payloads)
         rec = {"sf": sf, "snr_db": float(snr), "frames": frames, "ser": ser,
                "ber": float(np.unpackbits(diff).mean()), "per": float(diff.any(1).mean()),
-               "sync_ok": float((res.sync == 0x12).float().mean()), "cfo_bins": cfo_bins}
+               "sync_ok": float((res.sync == 0x12).float().mean()), "cfo_bins": cfo_bins,
+               "recomputed_symbols": int(plan.spec_recomputed() - fixed0)}
+        if xplan is not None:
+            rx_ = xplan.run(iq)
+            bad = ((res.symbols != rx_.symbols).any(1) | (res.sync != rx_.sync)
+                   | (res.cfo.view(torch.int32) != rx_.cfo.view(torch.int32))
+                   | (res.time_offset.view(torch.int32) != rx_.time_offset.view(torch.int32)))
+            rec["exact_path_frames_compared"] = frames
+            rec["exact_path_frame_mismatches"] = int(bad.sum())
         if keep_iq:
             rec["iq"] = iq
             rec["result"] = res

@@ -77,3 +77,20 @@ def test_chain_sweep_bit_exact_vs_oracle(awgn, sf, cfo):
         np.testing.assert_array_equal(got.time_offset.cpu().numpy().view(np.uint32), toff.view(np.uint32))
     if cfo == 0.0:
         assert recs[-1]["per"] == 0.0  # +10 dB, no CFO: every packet decodes
+
+
+@pytest.mark.parametrize("sf", [8, 11])
+def test_one_db_slice_every_frame_equals_exact_path(awgn, sf):
+    """configs[3] as SURVEY.md 8(d)4 states it, on a slice: -20 .. +10 dB in 1 dB steps with a
+    0.2-bin carrier offset; EVERY frame's symbols, sync word and cfo / time_offset bits from
+    the default pipeline equal the three-launch exact path's (the oracle-pinned kernels,
+    LORA_MI355X_SPEC=0).  The full sweep (SF 7-12, 1,000 frames per point) is
+    tools/awgn_sweep_gpu.py's record in profiles/r04/awgn_sweep.json."""
+    frames = 200 if sf < 11 else 60
+    snrs = [float(s) for s in range(-20, 11)]
+    recs = awgn.sweep_chain(sf, snrs, frames=frames, payload_len=16, seed=40 + sf, cfo_bins=0.2,
+                            exact_check=True)
+    bad = [(r["snr_db"], r["exact_path_frame_mismatches"]) for r in recs if r["exact_path_frame_mismatches"]]
+    assert not bad, bad
+    print(f"\nSF{sf}: {len(recs)} points x {frames} frames equal to the exact path; recomputed per point "
+          f"{[r['recomputed_symbols'] for r in recs]}")

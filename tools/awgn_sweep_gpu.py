@@ -8,7 +8,10 @@ agreement of every GPU output (symbols, sync, cfo/time_offset bits) with the CPU
 oracle on the first `--check` frames of each point.  Also the reference script's own
 model (awgn.simulate, RAW mode) at the same SNRs for SF7.
 
-usage: python tools/awgn_sweep_gpu.py [--frames 1000] [--snr -20 10 1] [--out FILE]
+usage: python tools/awgn_sweep_gpu.py [--frames 1000] [--snr -20 10 1] [--cfo 0.2] [--out FILE]
+
+Every frame of every point is also compared with the three-launch exact path (the
+oracle-pinned kernels, LORA_MI355X_SPEC=0): symbols, sync word and cfo / time_offset bits.
 """
 import argparse
 import json
@@ -45,7 +48,7 @@ def main():
     t0 = time.time()
     for sf in args.sfs:
         recs = awgn.sweep_chain(sf, snrs, frames=args.frames, payload_len=args.payload, seed=1234 + sf,
-                                cfo_bins=args.cfo, keep_iq=True)
+                                cfo_bins=args.cfo, keep_iq=True, exact_check=True)
         for r in recs:
             k = min(args.check, args.frames)
             x = r.pop("iq")[:k].cpu().numpy()
@@ -60,7 +63,8 @@ def main():
             r["oracle_bit_exact"] = bool(agree)
             out["chain"].append(r)
             print(f"SF{sf} {r['snr_db']:+5.1f} dB  SER {r['ser']:.4f}  BER {r['ber']:.5f}  PER {r['per']:.3f}"
-                  f"  oracle-exact {agree}", flush=True)
+                  f"  oracle-exact {agree}  vs exact path: {r['exact_path_frame_mismatches']} of "
+                  f"{r['exact_path_frames_compared']} frames differ, {r['recomputed_symbols']} recomputed", flush=True)
     up, down = awgn.make_chirps(7)
     np.random.seed(1234)
     for snr in snrs:
@@ -69,7 +73,13 @@ def main():
             out["script_model"].append({"sf": 7, "cr": cr, "snr_db": float(snr), "ber": ber, "per": per})
     out["seconds"] = time.time() - t0
     all_exact = all(r["oracle_bit_exact"] for r in out["chain"])
-    print(f"done in {out['seconds']:.1f} s; every checked point bit-exact vs oracle: {all_exact}")
+    mism = sum(r["exact_path_frame_mismatches"] for r in out["chain"])
+    out["summary"] = {"points": len(out["chain"]), "oracle_checked_frames_per_point": min(args.check, args.frames),
+                      "all_oracle_checked_frames_bit_exact": all_exact,
+                      "exact_path_frames_compared": sum(r["exact_path_frames_compared"] for r in out["chain"]),
+                      "exact_path_frame_mismatches": mism}
+    print(f"done in {out['seconds']:.1f} s; every checked point bit-exact vs oracle: {all_exact}; "
+          f"frames differing from the exact path: {mism}")
     if args.out:
         json.dump(out, open(args.out, "w"), indent=1)
 
