@@ -583,7 +583,8 @@ struct ConstTw1 {
 template <int SF, bool KEEP, bool FMA = false, bool TWL = false, bool PACK = false, bool CPRE = false,
           class HOOK = NoHook>
 __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr,
-                                            const cf* twl = nullptr, const int* cpre = nullptr, HOOK hook = HOOK{}) {
+                                            const cf* twl = nullptr, const int* cpre = nullptr, HOOK hook = HOOK{},
+                                            const cf* wbpre = nullptr) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
   constexpr bool WL = G::WAVE_LOCAL;
@@ -631,10 +632,8 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
       // TWL (speculative demod): pass B's twiddles two per 16-byte load (KArgs::twTB2)
       if constexpr (!std::is_same_v<HOOK, NoHook>) {
         // every group's twiddles first, then the hook, then the pass
-        constexpr int NT = G::RB == 16 ? 15 : 3;
-        cf wb[(P / G::RB) * NT];
-#pragma unroll
-        for (int gg = 0; gg < P / G::RB; ++gg) load_tw2<G::RB, G::MA_B>(wb + gg * NT, (l + T * gg) % G::MA_B, a.twTB2);
+        // (the caller, which installs the hook, loaded them earlier in its round: wbpre)
+        const cf* wb = wbpre;
         __builtin_amdgcn_sched_barrier(0);
         hook();
         __builtin_amdgcn_sched_barrier(0);
@@ -1441,6 +1440,12 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       float pm = 0.0f;
 #pragma unroll
       for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
+      // pass B's twiddle pairs, requested once the table pairs are consumed: they have the
+      // rotation and passes 1 and A to arrive
+      constexpr int NTB = G::RB == 16 ? 15 : 3;
+      cf wb[(P / G::RB) * NTB];
+#pragma unroll
+      for (int gg = 0; gg < P / G::RB; ++gg) load_tw2<G::RB, G::MA_B>(wb + gg * NTB, (lr + T * gg) % G::MA_B, a.twTB2);
       asm volatile("" : "+v"(pm));
       cf z[P];
       {
@@ -1459,7 +1464,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
 #pragma unroll
       for (int h = 0; h < G::G1; ++h) cpre[h] = d == 0 ? cown[h] : (int)(a.rev[lr + T * h] >> G::LOGR1);
       const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true, true, decltype(hook)>(
-          z, rows + (size_t)g * rowc, lr, a, nullptr, twl, cpre, hook);
+          z, rows + (size_t)g * rowc, lr, a, nullptr, twl, cpre, hook, wb);
       const uint32_t lbest = (uint32_t)lk;
       uint32_t best = lbest, sec = (uint32_t)(lk >> 32);
       spec_reduce<SF>(best, sec, pm, tid0, red3);
