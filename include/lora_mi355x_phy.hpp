@@ -5,7 +5,13 @@
  * A caller written against the reference's phy.hpp and <lora_phy/ChirpGenerator.hpp>
  * (e.g. tests/e2e_chain_test.cpp:54-117, runners/rx_runner.cpp:102-122) compiles
  * unchanged with -I<repo>/include/compat (whose lora_phy/phy.hpp and
- * lora_phy/ChirpGenerator.hpp only include this header) and links with -llora_mi355x.
+ * lora_phy/ChirpGenerator.hpp only include this header) and links with -llora_phy
+ * (liblora_phy.so, the drop-in over liblora_mi355x.so).  Loading liblora_phy.so sets up the
+ * GPU side once, before main (the HIP runtime, a private AQL queue with every kernel object
+ * resolved, LEGACY plans for SF 2-12 x both windows, buffers for frames of up to 1 M samples
+ * and a modulator staging area), so lora_modulate, lora_demod_init and lora_demodulate
+ * allocate nothing on the host (no_alloc_test.cpp:52-99).  LORA_MI355X_DROPIN_LAZY=1 in the
+ * environment skips that set-up (each call then sets up what it needs, allocating).
  * The functions keep the reference's names, argument meaning and return values; the
  * demodulation runs on the GPU:
  *
@@ -32,7 +38,8 @@
  * call), by its destructor.  Neither workspace may be copied.  Each call is synchronous,
  * host pointers in and out, like the reference's; lora_demodulate performs no host
  * allocation when the frame fits the max_samples given to lora_demod_init (the
- * reference's no_alloc_test.cpp:90-99 guard).  For batches of frames already in device
+ * reference's no_alloc_test.cpp:90-99 guard); with the load-time runtime, lora_demod_init
+ * (max_samples <= 1 M) and lora_modulate (<= 2 M output samples) do not either.  For batches of frames already in device
  * memory use lora_demod_batch (lora_mi355x.h) directly.
  */
 #ifndef LORA_MI355X_PHY_HPP
@@ -46,6 +53,10 @@
 #include <cstdint>
 
 struct lora_demod_plan;  // lora_mi355x.h
+
+/* 0 when liblora_phy.so's load-time runtime is up (the legacy calls then allocate nothing),
+ * else the set-up step that failed (csrc/lora_phy_dropin.hip). */
+extern "C" int lora_phy_dropin_status(void);
 
 namespace lora_phy {
 
@@ -101,6 +112,12 @@ struct device_state {
   void* stream{};    // hipStream_t
   void* aql{};       // lora::AqlQueue (csrc/lora_aql.hip); null: frames go through HIP
   int aql_status{};  // why there is no queue: 0, or the failing step's code (lora_internal.h)
+  // Borrowed from the drop-in library's load-time runtime (no allocation at init): a slot
+  // of preallocated buffers (dev / host / stream while they are the slot's), a shared plan,
+  // the shared AQL queue.  release() returns them instead of freeing them.
+  int slot{-1};
+  bool shared_plan{};
+  bool shared_aql{};
 };
 void release(device_state& d);
 }  // namespace detail

@@ -39,7 +39,7 @@ namespace lora {
 namespace {
 
 constexpr unsigned kSlotBytes = 1024;  // kernarg slot per packet (explicit + 256 hidden)
-constexpr int kCache = 32;
+constexpr int kCache = 256;  // kernel objects resolved (the drop-in's warm-up: every SF and window)
 constexpr int kMaxExec = 8;
 
 struct AqlKernel {
@@ -341,13 +341,16 @@ int aql_run(AqlQueue* Q, const LaunchRecord& r) {
     if (ks[i]->kernarg > kSlotBytes || (uint64_t)r.l[i].grid * r.l[i].block > 0xffffffffull) return -22;
   }
   hsa_queue_t* q = Q->q;
-  // Every call waits for its last packet, so the queue is idle here - unless an earlier call
-  // timed out with packets still queued or running: their kernarg slots, staging and
-  // completion signal must not be reused, so refuse before writing anything (-63; callers
-  // treat the queue as broken after a -62 and stop using it).
-  if (Q->broken || hsa_queue_load_read_index_scacquire(q) != hsa_queue_load_write_index_relaxed(q)) return -63;
+  // Every call waits for its last packet's completion, so no earlier kernel still runs
+  // (the packet processor may advance the read index a little later: only the ring's space
+  // is waited for below) - unless an earlier call timed out: then its kernarg slots, staging
+  // and completion signal may still be in use, so refuse before writing anything (-63;
+  // callers treat the queue as broken after a -62 and stop using it).
+  if (Q->broken) return -63;
   const uint64_t n = (uint64_t)r.n;
   const uint64_t base = hsa_queue_add_write_index_relaxed(q, n);
+  while (base + n - hsa_queue_load_read_index_scacquire(q) > q->size) {
+  }
   hsa_signal_store_relaxed(Q->done, 1);
   hsa_kernel_dispatch_packet_t* ring = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address);
   for (int i = 0; i < r.n; ++i) {

@@ -1132,11 +1132,11 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
   int prev = 0;
   HIP_TRY(hipGetDevice(&prev));
   if (prev != device) HIP_TRY(hipSetDevice(device));
-  hipLaunchKernelGGL(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, a);
+  // (lora::launch: recorded instead when the C++ drop-in dispatches on its AQL queue)
+  lora::launch(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, a);
   const int64_t chirps = frames * a.nchirp;
   const int64_t per_block = (int64_t)kModLanes * kModWaves;
-  hipLaunchKernelGGL(k_mod_samples, dim3((unsigned)((chirps + per_block - 1) / per_block)), dim3(per_block), 0, st,
-                     a);
+  lora::launch(k_mod_samples, dim3((unsigned)((chirps + per_block - 1) / per_block)), dim3(per_block), 0, st, a);
   hipError_t e = hipGetLastError();
   if (prev != device) hipSetDevice(prev);
   if (e != hipSuccess) return set_error(LORA_EIO, std::string("mod launch: ") + hipGetErrorString(e));

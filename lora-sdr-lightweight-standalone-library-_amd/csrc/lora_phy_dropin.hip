@@ -4,7 +4,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "../../include/lora_mi355x.h"
 #include "../../include/lora_mi355x_phy.hpp"
@@ -91,13 +93,70 @@ DevLayout layout(const lora_demod_plan* plan, size_t samples, size_t N) {
   return d;
 }
 
-// The plan for (sf, osr, window, bw, mode): kept while they match, recreated (the old one
-// destroyed) otherwise.  The reference passes osr per lora_demodulate call.
+// ---- the drop-in's load-time runtime (no_alloc_test.cpp:52-99) ---------------------------
+// The reference's routines allocate nothing once their caller's buffers exist
+// (phy.hpp:187-189).  Every HIP runtime call that creates state or enqueues work allocates
+// host memory, so the drop-in library sets the GPU side up when it is loaded - before the
+// caller's main - and its legacy calls then only borrow: lora_demod_init takes a slot of
+// preallocated buffers and a prebuilt plan, lora_demodulate and lora_modulate dispatch on
+// the private AQL queue (lora_aql.hip) whose kernel objects were all resolved here.
+constexpr int kSlots = 4;                          // workspaces initialised at once
+constexpr size_t kSlotSamples = size_t(1) << 20;   // frames of up to 1 M samples (8 MB)
+constexpr size_t kModSamples = size_t(1) << 21;    // lora_modulate outputs of up to 2 M samples
+constexpr size_t kModSyms = size_t(1) << 16;       // ... of up to 64 K symbols
+
+struct Runtime {
+  bool up = false;
+  int device = 0;
+  int status = 0;  // 0, or the set-up step that failed (lora_phy_dropin_status)
+  lora::AqlQueue* aql = nullptr;
+  lora_demod_plan* plans[13][2] = {};  // LEGACY, osr 1, 125 kHz, dechirped input: [sf][window]
+  struct Slot {
+    void* dev = nullptr;
+    void* host = nullptr;
+    void* stream = nullptr;
+    size_t bytes = 0, samples = 0;
+    bool busy = false;
+  } slots[kSlots];
+  void* mod_host = nullptr;  // pinned: symbols | IQ
+  std::mutex mu;             // the queue, the slots and the modulator staging
+};
+Runtime& rt() {
+  static Runtime r;
+  return r;
+}
+
+struct FrameOut;
+int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* samples, size_t count,
+                  FrameOut& out, int64_t nsym, const DevLayout& d);
+
+// A borrowed plan for (sf, osr, window, bw, mode), or null.
+lora_demod_plan* shared_plan(unsigned sf, unsigned osr, int window, unsigned bw_hz, int mode) {
+  Runtime& R = rt();
+  if (!R.up || sf < 2 || sf > 12 || osr != 1 || bw_hz != 125000 || mode != LORA_MODE_LEGACY || window < 0 ||
+      window > 1)
+    return nullptr;
+  return R.plans[sf][window];
+}
+
+// The plan for (sf, osr, window, bw, mode): kept while they match, otherwise the runtime's
+// (borrowed) or a new one (the old one destroyed unless borrowed).  The reference passes osr
+// per lora_demodulate call.
 bool ensure_plan(lora_phy::detail::device_state& g, unsigned sf, unsigned osr, int window, unsigned bw_hz,
                  int mode) {
   if (g.plan && g.sf == sf && g.plan_osr == osr && g.plan_window == window && g.plan_bw == bw_hz) return true;
-  if (g.plan) lora_demod_plan_destroy(g.plan);
+  if (g.plan && !g.shared_plan) lora_demod_plan_destroy(g.plan);
   g.plan = nullptr;
+  g.shared_plan = false;
+  if (lora_demod_plan* sp = shared_plan(sf, osr, window, bw_hz, mode)) {
+    g.plan = sp;
+    g.shared_plan = true;
+    g.sf = sf;
+    g.plan_osr = osr;
+    g.plan_window = window;
+    g.plan_bw = bw_hz;
+    return true;
+  }
   lora_demod_params p{};
   p.sf = sf;
   p.osr = osr;
@@ -125,8 +184,9 @@ bool ensure_buffers(lora_phy::detail::device_state& g, size_t samples) {
   const DevLayout d = layout(g.plan, want, size_t(1) << g.sf);
   if (g.dev && g.host && g.bytes >= d.total && g.samples >= samples) return true;
   if (g.stream) hipStreamSynchronize(static_cast<hipStream_t>(g.stream));
-  if (g.dev) hipFree(g.dev);
-  if (g.host) hipHostFree(g.host);
+  const bool slot_bufs = g.slot >= 0 && g.dev == rt().slots[g.slot].dev;  // the slot keeps them
+  if (g.dev && !slot_bufs) hipFree(g.dev);
+  if (g.host && !slot_bufs) hipHostFree(g.host);
   g.dev = g.host = nullptr;
   g.bytes = g.samples = 0;
   if (hipMalloc(&g.dev, d.total) != hipSuccess) {
@@ -187,6 +247,9 @@ int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* 
   if (rc < 0) return 0;
   if (rec.bad) return -1;
   if (rec.n > 0) {
+    // the runtime's queue is shared by every borrowing workspace: one dispatch at a time
+    std::unique_lock<std::mutex> lk(rt().mu, std::defer_lock);
+    if (g.shared_aql) lk.lock();
     const int e = lora::aql_run(static_cast<lora::AqlQueue*>(g.aql), rec);
     if (e != 0) return e;
   }
@@ -213,10 +276,13 @@ bool run_frame(lora_phy::detail::device_state& g, const std::complex<float>* sam
     if (r == 0) return false;  // lora_demod_batch itself refused the frame
     if (r == -62) {
       // timed out with packets possibly still running: they read the staging and workspace
-      // and write the outputs there, so the queue and both buffers are abandoned (leaked)
-      // and this and later frames take the HIP path on fresh buffers
+      // and write the outputs there, so the queue and both buffers are abandoned (leaked;
+      // a borrowed slot stays busy) and this and later frames take the HIP path on fresh
+      // buffers
       g.aql = nullptr;
+      g.shared_aql = false;
       g.aql_status = -62;
+      g.slot = -1;
       g.dev = g.host = nullptr;
       g.bytes = g.samples = 0;
       if (!ensure_buffers(g, std::max<size_t>(count, 1))) return false;
@@ -266,21 +332,69 @@ int window_code(lora_phy::window_type w) {
 namespace lora_phy {
 
 void detail::release(device_state& g) {
-  // A workspace destroyed after the HIP runtime has been torn down (static storage duration,
-  // destructors at exit) must not call into it: hipGetDevice failing means it is gone.
+  // Borrowed parts go back to the runtime (no runtime call, nothing freed); the rest is
+  // freed.  A workspace destroyed after the HIP runtime has been torn down (static storage
+  // duration, destructors at exit) must not call into it: hipGetDevice failing means it is
+  // gone.
+  Runtime& R = rt();
+  bool slot_bufs = false, slot_stream = false;
+  if (g.slot >= 0) {
+    Runtime::Slot& S = R.slots[g.slot];
+    slot_bufs = g.dev == S.dev;
+    slot_stream = g.stream == S.stream;
+    std::lock_guard<std::mutex> lk(R.mu);
+    S.busy = false;
+  }
+  const bool own = (g.stream && !slot_stream) || (g.aql && !g.shared_aql) || (g.dev && !slot_bufs) ||
+                   (g.host && !slot_bufs) || (g.plan && !g.shared_plan);
   int cur = 0;
-  if ((g.stream || g.aql || g.dev || g.host || g.plan) && hipGetDevice(&cur) != hipSuccess) {
+  if (!own || hipGetDevice(&cur) != hipSuccess) {
     g = device_state{};
     return;
   }
   if (g.stream) hipStreamSynchronize(static_cast<hipStream_t>(g.stream));
-  if (g.aql) lora::aql_destroy(static_cast<lora::AqlQueue*>(g.aql));
-  if (g.dev) hipFree(g.dev);
-  if (g.host) hipHostFree(g.host);
-  if (g.plan) lora_demod_plan_destroy(g.plan);
-  if (g.stream) hipStreamDestroy(static_cast<hipStream_t>(g.stream));
+  if (g.aql && !g.shared_aql) lora::aql_destroy(static_cast<lora::AqlQueue*>(g.aql));
+  if (g.dev && !slot_bufs) hipFree(g.dev);
+  if (g.host && !slot_bufs) hipHostFree(g.host);
+  if (g.plan && !g.shared_plan) lora_demod_plan_destroy(g.plan);
+  if (g.stream && !slot_stream) hipStreamDestroy(static_cast<hipStream_t>(g.stream));
   g = device_state{};
 }
+
+namespace {
+// lora_demod_init's allocation-free path: a free slot large enough for max_samples, the
+// runtime's plan for (sf, window) and its queue.
+bool borrow(detail::device_state& g, unsigned sf, int window, size_t max_samples) {
+  Runtime& R = rt();
+  lora_demod_plan* plan = shared_plan(sf, 1, window, 125000, LORA_MODE_LEGACY);
+  if (!plan || !R.aql) return false;
+  const size_t n = std::max<size_t>(max_samples, 3 * (size_t(1) << sf));
+  std::lock_guard<std::mutex> lk(R.mu);
+  for (int i = 0; i < kSlots; ++i) {
+    Runtime::Slot& S = R.slots[i];
+    if (S.busy || S.samples < n) continue;
+    S.busy = true;
+    g.device = R.device;
+    g.plan = plan;
+    g.shared_plan = true;
+    g.sf = sf;
+    g.plan_osr = 1;
+    g.plan_window = window;
+    g.plan_bw = 125000;
+    g.dev = S.dev;
+    g.host = S.host;
+    g.bytes = S.bytes;
+    g.samples = S.samples;
+    g.stream = S.stream;
+    g.aql = R.aql;
+    g.shared_aql = true;
+    g.aql_status = 0;
+    g.slot = i;
+    return true;
+  }
+  return false;
+}
+}  // namespace
 
 // ---------------------------------------------------------------------------------------
 // Legacy helpers (phy.hpp:158-215)
@@ -297,6 +411,8 @@ void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win, std
   ws->scratch = scratch;
   ws->scratch_len = max_samples;
   ws->metrics = lora_metrics{};
+  // the load-time runtime's slot, plan and queue: nothing to set up, nothing allocated
+  if (sf >= 2 && sf <= 12 && borrow(ws->gpu, sf, window_code(win), max_samples)) return;
   int dev = 0;
   hipGetDevice(&dev);
   ws->gpu.device = dev;
@@ -367,6 +483,25 @@ size_t lora_modulate(const uint16_t* symbols, size_t symbol_count, std::complex<
   if (sf < 2 || sf > 12) return 0;
   const size_t per = (symbol_count + 2) * (size_t(1) << sf) * osr;
   if (!out_samples || (symbol_count > 0 && !symbols)) return 0;
+  Runtime& R = rt();
+  if (R.up && R.aql && per <= kModSamples && symbol_count <= kModSyms) {
+    // the runtime's pinned staging (symbols | IQ), which the kernels read and write in place,
+    // and its queue: no HIP runtime call
+    std::lock_guard<std::mutex> lk(R.mu);
+    uint16_t* hs = static_cast<uint16_t*>(R.mod_host);
+    float* hiq = reinterpret_cast<float*>(static_cast<unsigned char*>(R.mod_host) + align256(kModSyms * 2));
+    if (symbol_count > 0) std::memcpy(hs, symbols, symbol_count * 2);
+    lora::LaunchRecord rec;
+    lora::t_launch_record = &rec;
+    const int64_t r = lora_mod_batch(sf, osr, static_cast<unsigned>(bw), amplitude, sync, hs, 1,
+                                     (int64_t)symbol_count, hiq, R.device, nullptr);
+    lora::t_launch_record = nullptr;
+    if (r >= 0 && !rec.bad && rec.n > 0 && lora::aql_run(R.aql, rec) == 0) {
+      std::memcpy(out_samples, hiq, per * 8);
+      return per;
+    }
+    // otherwise (a launch the queue does not take) the HIP path below
+  }
   // per-thread device staging, grown on demand and tied to the device it was allocated
   // on (the reference's lora_modulate takes no workspace)
   thread_local void* dev = nullptr;
@@ -569,3 +704,111 @@ int genChirp(std::complex<float>* samps, int N, int osr, int NN, float f0, bool 
   lora::host_gen_chirp(samps, N, osr, NN, f0, down, ampl, phaseAccum, bw_scale);
   return NN;
 }
+
+// ---------------------------------------------------------------------------------------
+// Load-time set-up of the runtime (see Runtime above).  Runs when liblora_phy.so is loaded,
+// before the caller's main; any failure leaves the runtime down (status names the step) and
+// every call on its own allocating path.
+// ---------------------------------------------------------------------------------------
+namespace {
+void runtime_setup() {
+  Runtime& R = rt();
+  const char* lazy = std::getenv("LORA_MI355X_DROPIN_LAZY");
+  if (lazy && lazy[0] == '1') {
+    R.status = 1;
+    return;
+  }
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    R.status = 2;
+    return;
+  }
+  if (hipGetDevice(&R.device) != hipSuccess) {
+    R.status = 3;
+    return;
+  }
+  for (int sf = 2; sf <= 12; ++sf)
+    for (int w = 0; w < 2; ++w) {
+      lora_demod_params p{};
+      p.sf = (unsigned)sf;
+      p.osr = 1;
+      p.bw_hz = 125000;
+      p.window = w;
+      p.dechirp = 0;  // lora_demodulate takes dechirped samples
+      p.mode = LORA_MODE_LEGACY;
+      p.device = R.device;
+      p.precision = LORA_PRECISION_EXACT;
+      if (lora_demod_plan_create(&p, &R.plans[sf][w]) != LORA_OK) {
+        R.plans[sf][w] = nullptr;
+        R.status = 4;
+        return;
+      }
+    }
+  // slot buffers: the largest layout over the plans for frames of kSlotSamples samples
+  size_t need = 0;
+  for (int sf = 2; sf <= 12; ++sf) need = std::max(need, layout(R.plans[sf][0], kSlotSamples, size_t(1) << sf).total);
+  for (Runtime::Slot& S : R.slots) {
+    hipStream_t st = nullptr;
+    if (hipMalloc(&S.dev, need) != hipSuccess || hipHostMalloc(&S.host, need, hipHostMallocDefault) != hipSuccess ||
+        hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+      R.status = 5;
+      return;
+    }
+    S.stream = st;
+    S.bytes = need;
+    S.samples = kSlotSamples;
+  }
+  if (hipHostMalloc(&R.mod_host, align256(kModSyms * 2) + kModSamples * 8, hipHostMallocDefault) != hipSuccess) {
+    R.status = 6;
+    return;
+  }
+  const int q = lora::aql_create(R.device, &R.aql);
+  if (q != 0) {
+    R.aql = nullptr;
+    R.status = q;
+    return;
+  }
+  R.up = true;
+  // one frame per plan and path through the queue (the spec pipeline: 3 symbols; the
+  // three-launch path: 1 symbol) and one modulation, so that every kernel object the
+  // legacy calls dispatch is resolved now, not inside a caller's call
+  lora_phy::detail::device_state g;
+  for (int sf = 2; sf <= 12 && R.up; ++sf)
+    for (int w = 0; w < 2 && R.up; ++w) {
+      if (!lora_phy::borrow(g, (unsigned)sf, w, 0)) {
+        R.status = 7;
+        R.up = false;
+        break;
+      }
+      const size_t N = size_t(1) << sf;
+      const DevLayout d = layout(g.plan, g.samples, N);
+      std::complex<float>* zeros =
+          reinterpret_cast<std::complex<float>*>(static_cast<unsigned char*>(g.host) + d.iq);
+      std::memset(zeros, 0, 3 * N * sizeof(std::complex<float>));
+      FrameOut o;
+      for (size_t len : {3 * N, N}) {
+        const int r = run_frame_aql(g, zeros, len, o, lora_demod_symbols_per_frame(g.plan, (int64_t)len), d);
+        if (r != 1) {
+          R.status = r == -1 ? -130 : (r == 0 ? -131 : r);
+          R.up = false;
+          break;
+        }
+      }
+      lora_phy::detail::release(g);
+    }
+  if (R.up) {
+    uint16_t syms[4] = {0, 1, 2, 3};
+    std::complex<float> out[6 * 4];
+    if (lora_phy::lora_modulate(syms, 4, out, 2, 1, lora_phy::bandwidth::bw_125, 1.0f, 0x12) != 6 * 4) {
+      R.status = 8;
+      R.up = false;
+    }
+  }
+}
+__attribute__((constructor)) void lora_phy_dropin_load() { runtime_setup(); }
+}  // namespace
+
+// 0 when the load-time runtime is up, else the step that failed (1: disabled by
+// LORA_MI355X_DROPIN_LAZY, 2: no HIP device, 3-6: plans / buffers, a negative aql_create
+// code, 7-8 / -13x: the warm-up)
+extern "C" int lora_phy_dropin_status(void) { return rt().status; }

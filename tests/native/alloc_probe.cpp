@@ -108,7 +108,8 @@ int main() {
     (void)hipStreamDestroy(st);
   }
   lora_phy::lora_demod_free(&ws);
-  std::printf("{\"roundtrip_ok\": %s, \"aql_queue\": %s, \"aql_status\": %d, \"lora_modulate_first\": %zu, \"lora_modulate_second\": %zu, "
+  std::printf("{\"dropin_status\": %d, ", lora_phy_dropin_status());
+  std::printf("\"roundtrip_ok\": %s, \"aql_queue\": %s, \"aql_status\": %d, \"lora_modulate_first\": %zu, \"lora_modulate_second\": %zu, "
               "\"lora_demod_init\": %zu, \"lora_demodulate\": [%zu, %zu, %zu], \"hip_steps_second_call\": "
               "{\"memcpy_h2d_pinned\": %zu, \"lora_demod_batch\": %zu, \"memcpy_d2h_pinned\": %zu, "
               "\"stream_sync\": %zu}}\n",

@@ -1,6 +1,7 @@
 """CPU: the C++ drop-in builds and links - include/lora_mi355x_phy.hpp compiles for a caller
 that includes the reference's header names (include/compat), and the programs the GPU
-tests run resolve every lora_phy:: symbol from liblora_mi355x.so."""
+tests run resolve every lora_phy:: symbol from liblora_phy.so (the drop-in library over
+liblora_mi355x.so)."""
 import os
 import shutil
 import subprocess
@@ -9,7 +10,7 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB = os.path.join(REPO, "lora-sdr-lightweight-standalone-library-_amd", "lora_phy_amd", "lib", "liblora_mi355x.so")
+LIB = os.path.join(REPO, "lora-sdr-lightweight-standalone-library-_amd", "lora_phy_amd", "lib", "liblora_phy.so")
 E2E = os.path.join(HERE, "native", "e2e_dropin")
 
 
@@ -39,7 +40,8 @@ def test_dropin_symbols_exported():
                 # the workspace API (phy.hpp:102-156)
                 "lora_phy::init(", "lora_phy::reset(", "lora_phy::encode(", "lora_phy::decode(",
                 "lora_phy::modulate(", "lora_phy::demodulate(", "lora_phy::estimate_offsets(",
-                "lora_phy::compensate_offsets(", "lora_phy::get_last_metrics(", "lora_phy::detail::release("):
+                "lora_phy::compensate_offsets(", "lora_phy::get_last_metrics(", "lora_phy::detail::release(",
+                "lora_phy_dropin_status"):
         assert any(sym in line and " T " in line for line in out.splitlines()), sym
 
 
@@ -47,7 +49,7 @@ def test_e2e_program_links():
     if not os.path.exists(E2E):
         pytest.skip("tests/native/e2e_dropin not built")
     r = subprocess.run(["ldd", E2E], capture_output=True, text=True)
-    assert "liblora_mi355x.so" in r.stdout and "not found" not in r.stdout, r.stdout
+    assert "liblora_phy.so" in r.stdout and "liblora_mi355x.so" in r.stdout and "not found" not in r.stdout, r.stdout
 
 
 def test_workspace_api_compiles_for_rx_runner_style_caller(tmp_path):
