@@ -29,13 +29,11 @@
 namespace lora {
 namespace {
 
-// Scalar fp32 only: packed v_pk_mul/add_f32 issue at about half the scalar rate on this
-// chip (tools/micro/pk_rate) and need operand-pairing moves, so for these VALU-bound
-// kernels the scalar forms are cheaper (measured: SF7 demod -7 %, SF12 demod -13 %;
-// tools/exp/variant_ab.sh).  Same IEEE operations either way, so results are unchanged.
-// The Makefile drops the packed-fp32-ops feature for this whole translation unit (a
-// per-kernel target attribute kept every non-force-inlined helper out of line).
-#define LORA_SCALAR_FP32
+// Packed fp32 (v_pk_*_f32) only where it is written explicitly: the certified path's complex
+// products and butterflies (lora_device.h).  The Makefile turns the compiler's own
+// vectorisers off for this translation unit: its SLP-packed pairs cost operand-pairing moves
+// (measured in round 1: SF7 demod -7 %, SF12 -13 % without them).  The same IEEE operations
+// either way, so exact results are unchanged.
 
 template <int SF>
 struct Geo {
@@ -163,9 +161,6 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 
 // In-register DIT stages over x[0..R): positions base + MA*u, group offset k < MA.
 // Radix-2 (optional, only with MA == 1) then radix-4 stages, as kf_work unwinds.
-#ifndef LORA_UNIT_TW
-#define LORA_UNIT_TW 1
-#endif
 // UNIT (argmax-only transforms with k == 0): the butterflies whose twiddles are all
 // tw[0] = (1, 0) skip the multiplies.  x*(1,0) = (a*1 - b*0, a*0 + b*1) equals x except
 // for the sign of a zero component, and a zero's sign never reaches a non-zero result
@@ -387,7 +382,6 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
     // speculative demod, LEGACY osr 1 with the fused dechirp: the table values two per
     // 16-byte load from KArgs::downP (same values, same products)
     const cf* __restrict__ xl = x + l;
-#if LORA_IQ_NT
     // each sample is read once: nontemporal loads leave the caches to the tables
     typedef float v2f __attribute__((ext_vector_type(2)));
     const v2f* __restrict__ xl2 = reinterpret_cast<const v2f*>(xl);
@@ -396,10 +390,6 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
       const v2f v = __builtin_nontemporal_load(xl2 + T * q);
       in[q] = cf{v.x, v.y};
     }
-#else
-#pragma unroll
-    for (int q = 0; q < P; ++q) in[q] = xl[T * q];
-#endif
     const float4* __restrict__ dp = reinterpret_cast<const float4*>(a.downP) + cg + l;
 #pragma unroll
     for (int pp = 0; pp < P / 2; ++pp) {
@@ -434,21 +424,6 @@ __device__ __forceinline__ void gather_points(const KArgs& a, const cf* __restri
 // (:158-160), and placement in pass-1 leaf order.
 // Speculative demod table access (A/B knobs): pass-A twiddles staged in LDS, pass-B
 // twiddles in slot pairs (KArgs::twTB2).
-#ifndef LORA_TWA_LDS
-#define LORA_TWA_LDS 1
-#endif
-#ifndef LORA_DECH_PAIR
-#define LORA_DECH_PAIR 1  // ... and the fused dechirp's table values in pairs (KArgs::downP)
-#endif
-#ifndef LORA_IQ_NT
-#define LORA_IQ_NT 1  // nontemporal sample loads in the paired-table gather (step -0.6 to -0.8 %)
-#endif
-#ifndef LORA_EST_TWB_PAIR
-#define LORA_EST_TWB_PAIR 1  // ... also in every other transform (estimate, recompute)
-#endif
-#ifndef LORA_TWB_PAIR
-#define LORA_TWB_PAIR 1  // ... and pass B's twiddles in slot pairs (KArgs::twTB2)
-#endif
 template <int SF, bool ROT, bool FAST = false, bool FMA = false>
 __device__ __forceinline__ void rotate_place(const cf* in, cf* z, float start, float rate,
                                              bool hann, const float* __restrict__ win, int l) {
@@ -591,9 +566,9 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
 #pragma unroll
   for (int h = 0; h < G::G1; ++h) {
     if constexpr (FMA)
-      pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP, FMA, ConstTw1<N>>(z + h * R1, 0, ConstTw1<N>{});
+      pass_regs<R1, G::R2FIRST, N, 1, !KEEP, FMA, ConstTw1<N>>(z + h * R1, 0, ConstTw1<N>{});
     else
-      pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP, FMA>(z + h * R1, 0, a.tw);
+      pass_regs<R1, G::R2FIRST, N, 1, !KEEP, FMA>(z + h * R1, 0, a.tw);
   }
   uint64_t key = 0;
   if constexpr (G::NPASS == 1) {
@@ -639,8 +614,7 @@ __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& 
         __builtin_amdgcn_sched_barrier(0);
         pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, true, TWL, PACK>(row, z, l, a.tw, key, a.twTB2, second, wb);
       } else {
-        pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, (TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR, TWL, PACK>(
-            row, z, l, a.tw, key, ((TWL || LORA_EST_TWB_PAIR) && LORA_TWB_PAIR) ? a.twTB2 : a.twTB, second);
+        pass_lds<G::RB, N, G::MA_B, SF, T, P, true, FMA, true, TWL, PACK>(row, z, l, a.tw, key, a.twTB2, second);
       }
     }
     if constexpr (KEEP) {
@@ -667,8 +641,8 @@ __device__ __forceinline__ void fft_key2(cf* z0, cf* z1, cf* row0, cf* row1, int
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
 #pragma unroll
   for (int h = 0; h < G::G1; ++h) {
-    pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP>(z0 + h * R1, 0, a.tw);
-    pass_regs<R1, G::R2FIRST, N, 1, LORA_UNIT_TW && !KEEP>(z1 + h * R1, 0, a.tw);
+    pass_regs<R1, G::R2FIRST, N, 1, !KEEP>(z0 + h * R1, 0, a.tw);
+    pass_regs<R1, G::R2FIRST, N, 1, !KEEP>(z1 + h * R1, 0, a.tw);
   }
   int c[G::G1];
 #pragma unroll
@@ -847,7 +821,7 @@ constexpr int demod_waves_per_eu() {
 // arithmetic.  Returns the number of staged values (0: off).
 template <int SF, bool SPEC>
 constexpr int demod_twl_entries() {
-  if constexpr (!SPEC || !LORA_TWA_LDS || SF < 6) {
+  if constexpr (!SPEC || SF < 6) {
     return 0;
   } else {
     using G = Geo<SF>;
@@ -875,7 +849,7 @@ constexpr size_t spec_lds_bytes() {
 // max(|I|,|Q|), which k_est_fast<SPEC = 2> uses to normalise, certify or recompute.
 template <int SF, int MODE, bool FAST = false, bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
-LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
+k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
   constexpr bool RAW = MODE == 3;
@@ -926,7 +900,7 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
     if (tid < NTW) tv = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
   }
   cf in[P], z[P];
-  if (SPEC && LORA_DECH_PAIR && MODE == 0 && a.downP)  // the speculative demod's scale is 1
+  if (SPEC && MODE == 0 && a.downP)  // the speculative demod's scale is 1
     gather_points<SF, true>(a, x, l, 1, N, cg, 1, true, 1.0f, in);
   else
     gather_points<SF>(a, x, l, osr, step, cg, legacy ? 1 : 2, dech, SPEC ? 1.0f : scale, in);
@@ -959,43 +933,6 @@ LORA_SCALAR_FP32 k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
   }
 }
 
-// Diagnostic build only (tools/build_variant.sh stamps -DLORA_STAMPS; never in the
-// product library): per wave of the speculative demod, the shader clock at the end of
-// each phase and the 100 MHz real-time clock at start and end, into a buffer of its own
-// that no code reads (lora_debug_stamps copies it out).  tools/stamps.py reads it.
-#ifdef LORA_STAMPS
-constexpr int kStampWaves = 1 << 17;
-__device__ unsigned long long g_stamps[kStampWaves * 8];
-__device__ unsigned long long g_stamps_est[3][kStampWaves * 8];  // [SPEC stage 0/1/2]
-__device__ __forceinline__ void stamp_to(unsigned long long* buf, int k, bool real) {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  if (real)
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  else
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  const unsigned wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if ((threadIdx.x & 63) == 0 && wv < (unsigned)kStampWaves) buf[(size_t)wv * 8 + k] = t;
-}
-#define LORA_ESTAMP(k, real) stamp_to(g_stamps_est[SPEC], k, real)
-__device__ __forceinline__ void stamp(int k, bool real) {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  if (real)
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  else
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  const unsigned wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if ((threadIdx.x & 63) == 0 && wv < (unsigned)kStampWaves) g_stamps[(size_t)wv * 8 + k] = t;
-}
-#define LORA_STAMP(k, real) \
-  if (first_round) stamp(k, real)
-#else
-#define LORA_STAMP(k, real)
-#define LORA_ESTAMP(k, real)
-#endif
 
 // ---- the speculative pipeline's symbol pass -----------------------------------------
 // k_spec_demod: every symbol of LEGACY osr-1 unwindowed frames (MODE 0: fused caller
@@ -1013,25 +950,13 @@ __device__ __forceinline__ void stamp(int k, bool real) {
 // blocks blockIdx.x, blockIdx.x + gstride, ... (gstride = the grid: a few workgroups per CU,
 // launch_spec_demod) - short waves (about 4 us at SF7) left the CUs half occupied between
 // one workgroup's end and the next one's start.
-#ifndef LORA_SPEC_PERSIST
-#define LORA_SPEC_PERSIST 1  // 1: wave-local geometries (SF <= 10), 2: every SF, 0: none
-#endif
-#ifndef LORA_SPEC_ALIGN
-#define LORA_SPEC_ALIGN 1  // aligned gathers with lane roles (wave-local geometries)
-#endif
-#ifndef LORA_SPEC_PF
-#define LORA_SPEC_PF 1  // next-block sample prefetch in the SF 6-9 data phase
-#endif
-#ifndef LORA_SPEC_RAWSQRT
-#define LORA_SPEC_RAWSQRT 1  // margins from v_sqrt_f32 instead of IEEE sqrtf (-0.5 %)
-#endif
 // OSRN: oversampled frames (LEGACY osr 2-4, a.osr at run time): a symbol's points are every
 // osr-th sample of its window (LoRaDemod.cpp:141-157 reads sym_samps[i * osr]), and the
 // window's other samples are read with them for the frame maximum, which the reference takes
 // over every sample (LoRaDemod.cpp:59-67) - the frame is still read once.
 template <int SF, int MODE, bool HANN = false, bool OSRN = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
-LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
+k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, SPW = G::SPW;
   constexpr bool WL = G::WAVE_LOCAL;
@@ -1048,7 +973,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   const int per = tot - 2;
   // (PF geometries, MODE 0) the dechirp table's pairs at table phase 0 - what every window
   // of a t_off = 0 frame reads - staged after the twiddles: dtl[p T + c] = downP[p (N + T) + c]
-  constexpr bool DTL = LORA_SPEC_PF && WL && G::NPASS == 2 && !OSRN && MODE == 0;
+  constexpr bool DTL = WL && G::NPASS == 2 && !OSRN && MODE == 0;
   float4* dtl = reinterpret_cast<float4*>(smem + spec_dtl_offset<SF>());
   if constexpr (NTW > 0) {
     const int tid = threadIdx.x;
@@ -1068,9 +993,8 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
 
   // one block: SYNC = false a data block (frame-uniform), true a sync block
   // b: the block; data blocks come with b = fb bpf + rb (the loop keeps the quotient)
-  auto run_block = [&](auto sync_c, int64_t b, int64_t fb, int rb, bool first_round) {
+  auto run_block = [&](auto sync_c, int64_t b, int64_t fb, int rb) {
     constexpr bool SYNC = decltype(sync_c)::value;
-    (void)first_round;  // the diagnostic stamps record a workgroup's first round
     // the lane index, opaque per round: left visible, the compiler hoists every lane
     // address out of the loop and keeps them live across it (more VGPRs, spills at SF12)
     int tid = threadIdx.x;
@@ -1078,8 +1002,6 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     const int g = SPW == 1 ? 0 : tid / T;  // slot in the workgroup (its LDS row)
     const int l = tid % T;                 // lane within the symbol
     const int gi = WL ? (g % SPB) : g;     // symbol within the block
-    LORA_STAMP(5, true);
-    LORA_STAMP(0, false);
     int64_t f, fu;  // the lane's frame; the block's first (wave-uniform)
     int s;          // symbol within the frame
     bool valid;
@@ -1142,7 +1064,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     // the lane takes 17 loads and selects.  The roles permute the lanes of each symbol, so
     // the LDS accesses (and their banks) of every instruction are the same set.
     constexpr int D = T < 8 ? T : 8;
-    constexpr bool AL = LORA_SPEC_ALIGN;
+    constexpr bool AL = true;
     const int d = AL ? (int)(base & (D - 1)) : 0;
     lr = AL ? ((l - d) & (T - 1)) : l;
     v2f ld[P + 1];
@@ -1191,7 +1113,6 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
     }
     }  // osr 1
-    LORA_STAMP(1, false);
     cf z[P];
     {
       v2f F[P];
@@ -1199,9 +1120,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       spec_rotate_place<SF, HANN>(in, z, F, a.win, lr);
     }
     asm volatile("" : "+v"(pm));
-    LORA_STAMP(2, false);
     const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true>(z, rows + (size_t)g * rowc, lr, a, nullptr, twl);
-    LORA_STAMP(3, false);
     // the symbol's best and runner-up keys over its lanes; the lane holding the best key
     // has the index (equal best keys in two lanes: a zero margin, so the symbol is
     // recomputed and overwritten)
@@ -1213,12 +1132,9 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
       constexpr int ML = G::NPASS == 2 ? G::MA_A : G::MA_B;
       const int o = (int)(best & 15u);  // ordinal u * NG + gg: bin = l + T gg + ML u
       const uint32_t idx = (uint32_t)(lr + T * (o % NG) + ML * (o / NG));
-      // IEEE sqrtf, or (LORA_SPEC_RAWSQRT) v_sqrt_f32: within 1 ulp, a denormal argument may
-      // give 0 (an absolute error below 2^-63); the certification's E and absolute term
-      // carry either
-      const float margin = LORA_SPEC_RAWSQRT
-                               ? __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec))
-                               : sqrtf(spec_key_value(best)) - sqrtf(spec_key_value(sec));
+      // v_sqrt_f32: within 1 ulp, a denormal argument may give 0 (an absolute error below
+      // 2^-63); the certification's E and absolute term carry it
+      const float margin = __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec));
       uint2* mg = reinterpret_cast<uint2*>(a.spec_marg) + f * tot + s;
       if constexpr (!SYNC) {
         if (lbest == best && a.syms) a.syms[f * a.sym_stride + (s - 2)] = (uint16_t)idx;
@@ -1227,8 +1143,6 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
         if (lbest == best) *mg = make_uint2(__float_as_uint(margin), idx);
       }
     }
-    LORA_STAMP(4, false);
-    LORA_STAMP(6, true);
     block_sync<WL>();  // the rows (and red3) are rewritten by the next round
   };
   int64_t grp0 = blockIdx.x;
@@ -1238,7 +1152,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   // loaded with the table pairs ahead of the prefetch, pass A's are in LDS - so no wait on
   // the current block's operands also waits for the next block's samples (vmcnt retires in
   // order).
-  constexpr bool PF = LORA_SPEC_PF && WL && G::NPASS == 2 && !OSRN;
+  constexpr bool PF = WL && G::NPASS == 2 && !OSRN;
   if constexpr (PF) {
     constexpr int D = T < 8 ? T : 8;
     const int tid0 = threadIdx.x;
@@ -1349,9 +1263,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
         constexpr int ML = G::MA_A;
         const int o = (int)(best & 15u);
         const uint32_t idx = (uint32_t)(lr + T * (o % NG) + ML * (o / NG));
-        const float margin = LORA_SPEC_RAWSQRT
-                                 ? __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec))
-                                 : sqrtf(spec_key_value(best)) - sqrtf(spec_key_value(sec));
+        const float margin = __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec));
         if (lbest == best && a.syms) a.syms[B.f * a.sym_stride + (B.s - 2)] = (uint16_t)idx;
         if (l == 0)
           reinterpret_cast<uint2*>(a.spec_marg)[B.f * tot + B.s] = make_uint2(__float_as_uint(margin), __float_as_uint(pm));
@@ -1363,7 +1275,7 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
   // samples are requested at pass B, after every vector load of the transform (the pass-1
   // positions and twiddles, pass B's twiddle pairs - all older, so waiting for them never
   // waits for the prefetch).  SF 11-12: a block is the workgroup's symbol.
-  constexpr bool PF3 = LORA_SPEC_PF && G::NPASS == 3 && !OSRN;
+  constexpr bool PF3 = G::NPASS == 3 && !OSRN;
   if constexpr (PF3) {
     constexpr int D = T < 8 ? T : 8;
     const int tid0 = threadIdx.x;
@@ -1489,9 +1401,9 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
     if (WL && b >= blocks) break;
     if (b < dblocks) {
       const int64_t fb = b / bpf;
-      run_block(std::false_type{}, b, fb, (int)(b - fb * bpf), grp == blockIdx.x);
+      run_block(std::false_type{}, b, fb, (int)(b - fb * bpf));
     } else {
-      run_block(std::true_type{}, b, 0, 0, grp == blockIdx.x);
+      run_block(std::true_type{}, b, 0, 0);
     }
   }
 }
@@ -1505,9 +1417,6 @@ LORA_SCALAR_FP32 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride
 // exactly as k_demod_fast does for the data symbols, giving the sync word.
 // Latency-bound (a few sequential transforms per frame): occupancy matters more than
 // ILP, so the register budget is capped at two waves per SIMD.
-#ifndef LORA_EST_PAIR
-#define LORA_EST_PAIR 1
-#endif
 template <int SF>
 struct EstGeo {
   static constexpr int T = Geo<SF>::T;
@@ -1515,7 +1424,7 @@ struct EstGeo {
   static constexpr int SPB = BLOCK / T;             // frames per block
   // symbols 0 and 1 transformed in lockstep (two LDS rows per frame)
   // (SF 7-8; SF 6 would spill)
-  static constexpr bool PAIR = LORA_EST_PAIR && SF >= 7 && Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2;
+  static constexpr bool PAIR = SF >= 7 && Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2;
 };
 
 // SPEC (the speculative single-read pipeline, LEGACY osr-1 unwindowed frames, see
@@ -1648,12 +1557,9 @@ __device__ __forceinline__ void certify_list(const KArgs& a, int64_t f, const Fr
   }
 }
 
-#ifndef LORA_EST_WAVES
-#define LORA_EST_WAVES 2
-#endif
 template <int SF, int MODE, int SPEC = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EstGeo<SF>::PAIR ? 2 : LORA_EST_WAVES)))
-LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+k_est_fast(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
   constexpr int SPB = (T >= 64 ? 256 : 64) / T;  // frames per block (block = max(T, 64))
@@ -1664,8 +1570,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   __shared__ uint64_t red[4];
   __shared__ FrameParams sp[SPB];
   const int tid = threadIdx.x;
-  LORA_ESTAMP(5, true);
-  LORA_ESTAMP(0, false);
   if (SPEC == 1 && blockIdx.x == 0 && tid < kFixStripes) a.fix_count[16 * tid] = 0;  // the reject list
   const int step = DYN ? a.step : N;
   const int osr = DYN ? a.osr : 1;
@@ -1698,15 +1602,14 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
   }
   const int scaled = maxv > 1.0f;
   const float scale = scaled ? 1.0f / maxv : 1.0f;
-  LORA_ESTAMP(1, false);
   if constexpr (SPEC == 2) {
     // max <= 1: no rescaling, so the pre-pass estimate and its sync word are already the
     // reference's (identical inputs and arithmetic); the symbols, rotated with the
     // hardware sine/cosine, go through the certification below like a rescaled frame's.
     if (!scaled) {
       if (l == 0 && valid) {
-        const FrameParams qs = a.fp_spec[f];
-        a.fp[f] = qs;
+        const FrameParams qs = load_fp(a.fp_spec + f);
+        store_fp(a.fp + f, qs);
         if (a.cfo) a.cfo[f] = qs.cfo;
         if (a.toff) a.toff[f] = qs.toff;
         if (a.max_amp) a.max_amp[f] = maxv;
@@ -1846,7 +1749,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
         have_prev = true;
       }
     }
-    LORA_ESTAMP(2, false);
     if (l == 0) {
       const float avg_index = sum_index / 2.0f;
       const float cfo_coarse = avg_index / (float)N;
@@ -1877,7 +1779,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     }
     block_sync<G::WAVE_LOCAL>();
     q = sp[g];
-    LORA_ESTAMP(3, false);
     if constexpr (SPEC == 1) {
       // The samples outside every data-symbol window of the pre-pass offsets: [0, start of
       // symbol 2's window) and [end of the last window, frame_len).  With the windows'
@@ -1905,8 +1806,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       (void)per;
       if (l == 0 && valid) a.spec_max[f] = (uint32_t)(mk >> 32);
       // The sync word waits for the exact offsets: k_est_fast<SPEC = 2> computes it.
-      LORA_ESTAMP(4, false);
-      LORA_ESTAMP(6, true);
       return;
     }
   }  // exact estimate
@@ -1943,7 +1842,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
       const unsigned shift = a.sf > 4 ? a.sf - 4 : 0;
       a.sync[f] = (uint8_t)((((sw[0] >> shift) & 0x0f) << 4) | ((sw[1] >> shift) & 0x0f));
     }
-    LORA_ESTAMP(4, false);
   }
   if constexpr (SPEC == 2) {
     // ---- certification of the data symbols the demod computed speculatively ----
@@ -1981,8 +1879,6 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
     // recomputed exactly with the reference's arithmetic by k_spec_fix, the pipeline's
     // fourth launch, across the whole GPU (lora_demod_spec_recomputed() counts them).
     certify_list<SF, T>(a, f, q, valid, l);
-    LORA_ESTAMP(7, false);
-    LORA_ESTAMP(6, true);
   }
 }
 
@@ -1996,7 +1892,7 @@ LORA_SCALAR_FP32 k_est_fast(KArgs a, int64_t frames, int rowc) {
 // list still spreads over every CU (slot g of round r: i = blockIdx.x + grid (r SPW + g)).
 template <int SF, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-LORA_SCALAR_FP32 k_spec_fix(KArgs a, int rowc, int64_t grid) {
+k_spec_fix(KArgs a, int rowc, int64_t grid) {
   using G = Geo<SF>;
   constexpr int T = G::T, SPW = G::SPW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2064,16 +1960,9 @@ int row_complex() {
 // registers each: the pre-pass is a latency-bound chain per frame (SF7: 13.7 vs 15-18 us).
 // The same split of stage 2 (exact estimate + certification) measured slower - 47.7 vs
 // 28-35 us, its certification state needs the registers - and was removed.
-#ifndef LORA_EST_SPLIT
-#define LORA_EST_SPLIT 1
-#endif
-#ifndef LORA_CERT_SPLIT
-#define LORA_CERT_SPLIT 1  // stage 2 in the same layout (k_cert_split)
-#endif
 template <int SF, int MODE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
-LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
-  [[maybe_unused]] constexpr int SPEC = 1;  // LORA_ESTAMP's stage
+k_est_split(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
   constexpr int FPW = 64 / (2 * T);  // frames per wave (= block)
@@ -2083,8 +1972,6 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
   __shared__ FrameParams sp[FPW];
   __shared__ float tail[FPW][2][4];  // per frame and symbol: index, fractional index, phase, -
   const int tid = threadIdx.x;
-  LORA_ESTAMP(5, true);
-  LORA_ESTAMP(0, false);
   if (blockIdx.x == 0 && tid < kFixStripes) a.fix_count[16 * tid] = 0;  // the certification's reject list
   const int g2 = tid / T;     // lane group: frame slot fg, symbol sym
   const int fg = g2 >> 1;
@@ -2106,7 +1993,6 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
   // frame maximum is only known after the symbol pass)
   const int scaled = 0;
   const float scale = 1.0f;
-  LORA_ESTAMP(1, false);
   FrameParams q;
   {
     // LoRaDemod.cpp:79-123 (osr 1: one phase per symbol) for symbol `sym` of the frame
@@ -2133,7 +2019,6 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
       tail[fg][sym][2] = lm_atan2f(take ? B.im : 0.0f, take ? B.re : 0.0f);
     }
     wave_sync();
-    LORA_ESTAMP(2, false);
     if (l2 == 0) {
       // LoRaDemod.cpp:105-135 in the reference's order: symbol 0's terms, then symbol 1's
       float sum_index = 0.0f, phase_diff = 0.0f;
@@ -2163,7 +2048,6 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
     }
     wave_sync();
     q = sp[fg];
-    LORA_ESTAMP(3, false);
     {
       // the samples outside every data-symbol window of these offsets: [0, 2N) came with
       // the gathers above; a positive t_off's [2N, 2N + t_off) and the frame's tail here
@@ -2187,8 +2071,6 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
       if (l2 == 0 && valid) a.spec_max[f] = __float_as_uint(m);
       // the sync word waits for the exact offsets (k_est_fast<SPEC = 2>)
     }
-    LORA_ESTAMP(4, false);
-    LORA_ESTAMP(6, true);
   }
 }
 
@@ -2201,8 +2083,7 @@ LORA_SCALAR_FP32 k_est_split(KArgs a, int64_t frames, int rowc) {
 // certification of every speculative symbol over the frame's 2T lanes (certify_list).
 template <int SF, int MODE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
-LORA_SCALAR_FP32 k_cert_split(KArgs a, int64_t frames, int rowc) {
-  [[maybe_unused]] constexpr int SPEC = 2;  // LORA_ESTAMP's stage
+k_cert_split(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
   constexpr int FPW = 64 / (2 * T);  // frames per wave (= block)
@@ -2212,8 +2093,6 @@ LORA_SCALAR_FP32 k_cert_split(KArgs a, int64_t frames, int rowc) {
   __shared__ FrameParams sp[FPW];
   __shared__ float tail[FPW][2][4];  // per frame and symbol: index, fractional index, phase, -
   const int tid = threadIdx.x;
-  LORA_ESTAMP(5, true);
-  LORA_ESTAMP(0, false);
   const int g2 = tid / T;  // lane group: frame slot fg, symbol sym
   const int fg = g2 >> 1;
   const int sym = g2 & 1;
@@ -2245,16 +2124,15 @@ LORA_SCALAR_FP32 k_cert_split(KArgs a, int64_t frames, int rowc) {
 #pragma unroll
     for (int q = 0; q < P; ++q) in[q] = cscale(in[q], scale);
   }
-  LORA_ESTAMP(1, false);
   // A wave whose frames are all unscaled (max <= 1) takes the pre-pass estimate as it is
   // (identical inputs and arithmetic); any other computes the exact estimate for all its
   // frames (an unscaled one's equals the pre-pass's).
   if (__builtin_amdgcn_readfirstlane(__ballot(scaled) == 0)) {
     if (l2 == 0) {
-      const FrameParams qs = a.fp_spec[f];
-      sp[fg] = qs;
+      const FrameParams qs = load_fp(a.fp_spec + f);
+      store_fp(sp + fg, qs);
       if (valid) {
-        a.fp[f] = qs;
+        store_fp(a.fp + f, qs);
         if (a.cfo) a.cfo[f] = qs.cfo;
         if (a.toff) a.toff[f] = qs.toff;
         if (a.max_amp) a.max_amp[f] = maxv;
@@ -2281,7 +2159,6 @@ LORA_SCALAR_FP32 k_cert_split(KArgs a, int64_t frames, int rowc) {
       }
       wave_sync();
     }
-    LORA_ESTAMP(2, false);
     if (l2 == 0) {
       // LoRaDemod.cpp:105-135 in the reference's order: symbol 0's terms, then symbol 1's
       float sum_index = 0.0f, phase_diff = 0.0f;
@@ -2317,10 +2194,7 @@ LORA_SCALAR_FP32 k_cert_split(KArgs a, int64_t frames, int rowc) {
   }
   wave_sync();
   const FrameParams q = sp[fg];
-  LORA_ESTAMP(3, false);
   certify_list<SF, 2 * T>(a, f, q, valid, l2);
-  LORA_ESTAMP(7, false);
-  LORA_ESTAMP(6, true);
 }
 
 template <int SF, int MODE>
@@ -2388,11 +2262,9 @@ bool launch_mode(const KArgs& a, int s0, int64_t work, hipStream_t st) {
   return true;
 }
 
+constexpr int kSpecWgPerCu = 4;
 // Persistent grid of the speculative demod: kSpecWgPerCu workgroups per CU (the LDS rows
 // allow four at every SF), or one per group when there are fewer groups.
-#ifndef LORA_SPEC_WG_PER_CU
-#define LORA_SPEC_WG_PER_CU 4
-#endif
 int device_cus() {
   static int cache[64] = {};
   int dev = 0;
@@ -2421,9 +2293,8 @@ bool launch_spec_demod_w(const KArgs& a, int64_t frames, hipStream_t st) {
   const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB) + (2 * frames + SPB - 1) / SPB;
   const int64_t groups = (blocks + BPG - 1) / BPG;
   // persistent: the wave-local geometries, and every prefetching one (PF3: SF 10-12)
-  const bool persist = LORA_SPEC_PERSIST == 2 || (LORA_SPEC_PERSIST == 1 && G::WAVE_LOCAL) ||
-                       (LORA_SPEC_PF && G::NPASS == 3 && a.osr == 1);
-  const int64_t cap = persist ? (int64_t)device_cus() * LORA_SPEC_WG_PER_CU : groups;
+  const bool persist = G::WAVE_LOCAL || (G::NPASS == 3 && a.osr == 1);
+  const int64_t cap = persist ? (int64_t)device_cus() * kSpecWgPerCu : groups;
   const int64_t grid = groups < cap ? groups : cap;
   launch(k_spec_demod<SF, MODE, HANN, OSRN>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
   return true;
@@ -2471,9 +2342,9 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
       if (stage == 2) return launch_est_mode<SF, 2, 2>(a, frames, st);
       return launch_spec_fix<SF, 2>(a, frames, st);
     }
-    if constexpr (SF <= 9 && LORA_EST_SPLIT) {
+    if constexpr (SF <= 9) {
       if (stage == 0) return a.dechirp ? launch_est_split<SF, 0>(a, frames, st) : launch_est_split<SF, 1>(a, frames, st);
-      if (stage == 2 && LORA_CERT_SPLIT)
+      if (stage == 2)
         return a.dechirp ? launch_cert_split<SF, 0>(a, frames, st) : launch_cert_split<SF, 1>(a, frames, st);
     }
     if (stage == 3) return a.dechirp ? launch_spec_fix<SF, 0>(a, frames, st) : launch_spec_fix<SF, 1>(a, frames, st);
@@ -2500,21 +2371,6 @@ bool launch_sf(const KArgs& a, int s0, int64_t work, hipStream_t st) {
 
 }  // namespace
 
-#ifdef LORA_STAMPS
-extern "C" int lora_debug_stamps(unsigned long long* host, size_t n) {
-  n = n < (size_t)kStampWaves * 8 ? n : (size_t)kStampWaves * 8;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -5;
-}
-// stage 0 / 1 / 2 of the estimate kernels (k_est_fast<SF, MODE, SPEC = stage>)
-extern "C" int lora_debug_stamps_est(int stage, unsigned long long* host, size_t n) {
-  n = n < (size_t)kStampWaves * 8 ? n : (size_t)kStampWaves * 8;
-  if (stage < 0 || stage > 2) return -22;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_est), n * sizeof(unsigned long long),
-                             (size_t)stage * kStampWaves * 8 * sizeof(unsigned long long)) == hipSuccess
-             ? 0
-             : -5;
-}
-#endif
 
 bool launch_spec(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   switch (a.sf) {

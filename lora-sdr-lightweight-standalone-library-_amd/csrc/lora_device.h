@@ -27,6 +27,30 @@ struct FrameParams {
   float cfo, toff, rate, scale;
   int t_off, scaled, pad0, pad1;
 };
+// Field by field: a whole-struct copy between global and LDS memory was lowered through a
+// 32-byte scratch buffer (k_cert_split, k_est_fast<..., 2>).
+__device__ __forceinline__ FrameParams load_fp(const FrameParams* p) {
+  FrameParams q;
+  q.cfo = p->cfo;
+  q.toff = p->toff;
+  q.rate = p->rate;
+  q.scale = p->scale;
+  q.t_off = p->t_off;
+  q.scaled = p->scaled;
+  q.pad0 = p->pad0;
+  q.pad1 = p->pad1;
+  return q;
+}
+__device__ __forceinline__ void store_fp(FrameParams* p, const FrameParams& q) {
+  p->cfo = q.cfo;
+  p->toff = q.toff;
+  p->rate = q.rate;
+  p->scale = q.scale;
+  p->t_off = q.t_off;
+  p->scaled = q.scaled;
+  p->pad0 = q.pad0;
+  p->pad1 = q.pad1;
+}
 
 // std::complex<float> product as GCC lowers it: (ac - bd, ad + bc).
 __device__ __forceinline__ cf cmul(cf a, cf b) {
