@@ -512,7 +512,7 @@ def roofline(r, probe=None):
             "bytes_per_launch": r["dominant_bytes_per_launch"],
             "traffic": pmc_dom,
             "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch, "
-                              "tools/pmc_r03.py; committed, not measured in this run)",
+                              "tools/pmc_r04.py; committed, not measured in this run)",
             # the kernel's other roof: VALU issue (SQ_INSTS_VALU x 4 cycles over 1024 SIMDs x the
             # GRBM-measured cycles of the same launch, committed profile)
             "valu": {"busy_frac": load_pmc(wl, "valu_busy_frac"),
@@ -628,6 +628,10 @@ def main():
             line["symbol_pass_gbs"] = ro["dominant_gbs"]
             line["symbol_pass_frac"] = ro["dominant_gbs"] / HBM_PEAK_GBS
             line["step_bytes"] = ro["step_bytes"]
+            # HBM bytes the counters saw per symbol-pass launch over its algorithmic bytes
+            # (committed rocprofv3 FETCH_SIZE / WRITE_SIZE profile, tools/pmc_r04.py)
+            line["symbol_pass_counter_over_algorithmic"] = load_pmc(f"osr{osr}_sf7", "traffic_over_algorithmic")
+            line["step_counter_over_algorithmic"] = load_pmc(f"osr{osr}_sf7", "step_traffic_over_algorithmic")
             if osr == 2:
                 rt = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank,
                                 osr=osr, inputs=(ro["syms"], ro["iq"]), spec=False)
@@ -672,7 +676,10 @@ def main():
         del r12
         torch.cuda.empty_cache()
         if not args.no_variants:
-            extra["mod_sf12"] = run_modulator(12, 2000, args.data_symbols, device)
+            # the SF12 batch's shape (15,625 frames): the modulator's time is set by each
+            # frame's sequential phase chain (k_mod_phase), so a smaller batch only measures
+            # that chain's length
+            extra["mod_sf12"] = run_modulator(12, args.sf12_frames, args.data_symbols, device)
     if not args.no_channels:
         extra["channels"] = run_channels(args.channel_frames, 16, max(args.steps // 4, 2), 1, dist, device, rank)
         torch.cuda.empty_cache()

@@ -537,6 +537,7 @@ __global__ void __launch_bounds__(256) k_compensate(const cf* __restrict__ in, c
 // ---------------------------------------------------------------------------------
 struct ModArgs {
   int N, osr, step, nchirp;
+  int fpw;  // k_mod_phase: frames per 64-lane wave (lanes >= fpw idle)
   float fMin, fMax, fStep, ampl, bw_scale;
   uint16_t sw0, sw1;
   const uint16_t* syms;
@@ -550,8 +551,43 @@ __device__ __forceinline__ float chirp_f0(const ModArgs& a, int64_t frame, int c
   return (2.0f * PI_F * (float)(int)v * a.bw_scale) / ((float)a.N * (float)a.osr);
 }
 
+// K steps of the genChirp recurrence (ChirpGenerator.hpp:118-128: f += fStep, wrap at
+// fMax, phase += f, all fp32), speculatively without the wrap: fStep > 0, so f only grows
+// between wraps and the K unwrapped steps are the recurrence's own exactly when the last
+// f stays <= fMax; otherwise (once per chirp) the K steps are redone with the wrap.  Two
+// VALU operations per step instead of five.  ph[k] (optional) receives the phases.
+template <int K>
+__device__ __forceinline__ void chirp_steps(float& f, float& phase, float fStep, float fMax, float span, float* ph) {
+  float ft = f, pt = phase;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    ft += fStep;
+    pt += ft;
+    if (ph) ph[k] = pt;
+  }
+  if (ft > fMax) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      f += fStep;
+      f = f > fMax ? f - span : f;
+      phase += f;
+      if (ph) ph[k] = phase;
+    }
+  } else {
+    f = ft;
+    phase = pt;
+  }
+}
+
+// The start phase of every chirp of a frame: one lane per frame runs the frame's whole
+// chain (sequential by construction: each chirp starts from the previous one's wrapped end
+// phase).  For long chirps the chain's length, not the work, sets the kernel's time, so the
+// frames are spread a.fpw per wave over about a thousand waves (at most one per SIMD), which
+// also keeps chirp_steps' redo (a lane's wrap in a block) rare per wave (SF12, 15,625 frames:
+// 3.47 -> ms).
 __global__ void k_mod_phase(ModArgs a) {
-  const int64_t fr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int)threadIdx.x >= a.fpw) return;
+  const int64_t fr = (int64_t)blockIdx.x * a.fpw + threadIdx.x;
   if (fr >= a.frames) return;
   cf* out = a.iq + fr * (int64_t)a.nchirp * a.step;
   float phase = 0.0f;
@@ -559,14 +595,16 @@ __global__ void k_mod_phase(ModArgs a) {
   for (int c = 0; c < a.nchirp; ++c) {
     out[(int64_t)c * a.step].re = phase;  // start phase, consumed by k_mod_samples
     float f = a.fMin + chirp_f0(a, fr, c);
-    // One lane per frame runs the whole chain: the kernel is bound by this loop's
-    // instruction count (one wave per SIMD issues a wave64 VALU op every 4 cycles), so
-    // it is unrolled - 5 VALU per sample, no scalar loop overhead (SF12: 7.9 -> ~3 ms).
-#pragma unroll 16
-    for (int i = 0; i < a.step; ++i) {
-      f += a.fStep;
-      f = f > a.fMax ? f - span : f;
-      phase += f;
+    // (a wave redoes a block when any of its fpw lanes wraps in it: one block in step / 16
+    // per lane, so only long chirps gain)
+    if (a.step >= 1024 && a.step % 16 == 0) {
+      for (int i = 0; i < a.step; i += 16) chirp_steps<16>(f, phase, a.fStep, a.fMax, span, nullptr);
+    } else {
+      for (int i = 0; i < a.step; ++i) {
+        f += a.fStep;
+        f = f > a.fMax ? f - span : f;
+        phase += f;
+      }
     }
     phase = (float)((double)phase - floor((double)phase / (2 * M_PI)) * 2 * M_PI);
   }
@@ -603,11 +641,16 @@ __global__ void __launch_bounds__(kModLanes * kModWaves) k_mod_samples(ModArgs a
   const int sub = lane >> 4, j = lane & (kModBatch - 1);
   for (int i0 = 0; i0 < a.step; i0 += kModBatch) {
     const int cnt = min(kModBatch, a.step - i0);
-    for (int k = 0; k < cnt; ++k) {
-      f += a.fStep;
-      if (f > a.fMax) f -= span;
-      phase += f;
-      tile[lane][k] = phase;
+    // (64 chirps per wave: the speculation pays only when a wave's blocks rarely hold a wrap)
+    if (cnt == kModBatch && a.step >= 4096) {
+      chirp_steps<kModBatch>(f, phase, a.fStep, a.fMax, span, tile[lane]);
+    } else {
+      for (int k = 0; k < cnt; ++k) {
+        f += a.fStep;
+        if (f > a.fMax) f -= span;
+        phase += f;
+        tile[lane][k] = phase;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1025,9 +1068,10 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   //   2. every symbol with those offsets on unscaled samples (k_spec_demod), which also
   //      reduces each data window's max(|I|,|Q|) - the frame-max pass's work, from the same
   //      read - and records each symbol's argmax margin;
-  //   3. the exact estimate from the assembled maximum (k_est_fast<SPEC=2>): outputs, and
-  //      each speculative symbol - sync symbols included - either certified (its margin
-  //      exceeds the rounding bound, so the reference's argmax is the same bin) or listed;
+  //   3. the exact estimate from the assembled maximum (k_est_fast<SPEC=2>; SF 6-9
+  //      k_cert_split): outputs, and each speculative symbol - sync symbols included -
+  //      either certified (its margin exceeds the rounding bound, so the reference's argmax
+  //      is the same bin) or listed;
   //   4. the listed symbols and sync words recomputed exactly (k_spec_fix).
   // The IQ is read once plus symbols 0/1 twice; lora_demod_spec_recomputed() counts
   // recomputations.  The symbol demod rotates with the hardware sine/cosine under either
@@ -1133,7 +1177,12 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
   HIP_TRY(hipGetDevice(&prev));
   if (prev != device) HIP_TRY(hipSetDevice(device));
   // (lora::launch: recorded instead when the C++ drop-in dispatches on its AQL queue)
-  lora::launch(k_mod_phase, dim3((unsigned)((frames + 63) / 64)), dim3(64), 0, st, a);
+  // k_mod_phase: long chirps (the speculative blocks, step >= 1024) over about 1024 waves
+  // (frames per wave a power of two <= 64: fewer lanes per wave, fewer redone blocks);
+  // short ones 64 frames per wave (their chains are short: the lanes' issue count matters)
+  a.fpw = step >= 1024 ? 1 : 64;
+  while (a.fpw < 64 && (int64_t)a.fpw * 1024 < frames) a.fpw *= 2;
+  lora::launch(k_mod_phase, dim3((unsigned)((frames + a.fpw - 1) / a.fpw)), dim3(64), 0, st, a);
   const int64_t chirps = frames * a.nchirp;
   const int64_t per_block = (int64_t)kModLanes * kModWaves;
   lora::launch(k_mod_samples, dim3((unsigned)((chirps + per_block - 1) / per_block)), dim3(per_block), 0, st, a);

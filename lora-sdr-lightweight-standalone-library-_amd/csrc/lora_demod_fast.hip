@@ -950,11 +950,13 @@ k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
 // blocks blockIdx.x, blockIdx.x + gstride, ... (gstride = the grid: a few workgroups per CU,
 // launch_spec_demod) - short waves (about 4 us at SF7) left the CUs half occupied between
 // one workgroup's end and the next one's start.
-// OSRN: oversampled frames (LEGACY osr 2-4, a.osr at run time): a symbol's points are every
-// osr-th sample of its window (LoRaDemod.cpp:141-157 reads sym_samps[i * osr]), and the
-// window's other samples are read with them for the frame maximum, which the reference takes
-// over every sample (LoRaDemod.cpp:59-67) - the frame is still read once.
-template <int SF, int MODE, bool HANN = false, bool OSRN = false>
+// OSRV != 1: oversampled frames (LEGACY osr 2-4): a symbol's points are every osr-th sample
+// of its window (LoRaDemod.cpp:141-157 reads sym_samps[i * osr]), and the window's other
+// samples are read with them for the frame maximum, which the reference takes over every
+// sample (LoRaDemod.cpp:59-67) - the frame is still read once.  OSRV 2 / 4: osr known at
+// compile time, a point's osr samples in one / two 16-byte loads; OSRV 0: a.osr at run time
+// (osr 3, and the Hann window), one 8-byte load per sample.
+template <int SF, int MODE, bool HANN = false, int OSRV = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   using G = Geo<SF>;
@@ -963,7 +965,9 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   constexpr int SPB = WL ? 64 / T : SPW;  // symbols per block
   constexpr int BPG = WL ? 4 : 1;         // blocks per workgroup round
   constexpr int NTW = demod_twl_entries<SF, true>();
+  constexpr bool OSRN = OSRV != 1;
   static_assert(P == 16 && (MODE == 0 || MODE == 1), "SF >= 6, LEGACY (osr 1, or OSRN)");
+  static_assert(OSRV == 0 || OSRV == 1 || OSRV == 2 || OSRV == 4, "osr 1, 2, 4 or run time");
   static_assert(NTW <= 256, "one staged twiddle per thread");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t red3[3 * 4];  // spec_reduce's cross-wave words (T > 64)
@@ -1034,13 +1038,34 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
     if constexpr (OSRN) {
       // point q of lane l is sample base + (l + T q) osr; the osr samples from it on are
       // dechirped (MODE 0: table down[cg + j], no wrap) and enter the window's maximum
-      const int osr = a.osr;
+      const int osr = OSRV ? OSRV : a.osr;
       const __amdgpu_buffer_rsrc_t rx =
           __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + fu * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
       const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)a.down, (short)0, 0x7fffffff, 0x00020000);
       const int vo = rel + (int)(base + (int64_t)l * osr) * 8;
       const int vt = (cg + l * osr) * 8;
       const int so = T * osr * 8;  // bytes between a lane's points
+      if constexpr (OSRV == 2 || OSRV == 4) {
+        // the point's osr consecutive samples (and table values) two per 16-byte load: every
+        // byte of the window is fetched by exactly one load (8-byte loads of every osr-th
+        // sample, osr of them over the same lines, cost 1.31x the window's bytes at osr 2
+        // and 0.75 ms per 15,625-frame SF7 step against 0.41)
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+#pragma unroll
+          for (int h = 0; h < OSRV / 2; ++h) {
+            const float4 y2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo + 16 * h, q * so, 2 /* nt */));
+            cf y0 = cf{y2.x, y2.y}, y1 = cf{y2.z, y2.w};
+            if constexpr (MODE == 0) {
+              const float4 d2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vt + 16 * h, q * so, 0));
+              y0 = pk_cmul_ref(y0, cf{d2.x, d2.y});
+              y1 = pk_cmul_ref(y1, cf{d2.z, d2.w});
+            }
+            if constexpr (!SYNC) pm = amax3(amax3(pm, y0), y1);
+            if (h == 0) in[q] = y0;
+          }
+        }
+      } else {
 #pragma unroll
       for (int q = 0; q < P; ++q) {
         for (int k = 0; k < osr; ++k) {
@@ -1050,6 +1075,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
           if constexpr (!SYNC) pm = amax3(pm, y);
           if (k == 0) in[q] = y;
         }
+      }
       }
     } else {
     // The window's samples (read once: nontemporal) through a buffer resource on the
@@ -2277,14 +2303,14 @@ int device_cus() {
   return cache[dev];
 }
 
-template <int SF, int MODE, bool HANN, bool OSRN>
+template <int SF, int MODE, bool HANN, int OSRV>
 bool launch_spec_demod_w(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
   const size_t lds = spec_lds_bytes<SF>();
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN, OSRN>,
+    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN, OSRV>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return false;
   // the kernel's blocks: SPB symbols of one frame (see k_spec_demod), BPG per workgroup round
@@ -2296,18 +2322,21 @@ bool launch_spec_demod_w(const KArgs& a, int64_t frames, hipStream_t st) {
   const bool persist = G::WAVE_LOCAL || (G::NPASS == 3 && a.osr == 1);
   const int64_t cap = persist ? (int64_t)device_cus() * kSpecWgPerCu : groups;
   const int64_t grid = groups < cap ? groups : cap;
-  launch(k_spec_demod<SF, MODE, HANN, OSRN>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
+  launch(k_spec_demod<SF, MODE, HANN, OSRV>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
   return true;
 }
 // the Hann window (LoRaDemod.cpp:158-160) and oversampling as instantiations of their own:
 // the unwindowed osr-1 kernels keep no per-point branch
 template <int SF, int MODE>
 bool launch_spec_demod(const KArgs& a, int64_t frames, hipStream_t st) {
-  if (a.osr > 1)
-    return a.hann ? launch_spec_demod_w<SF, MODE, true, true>(a, frames, st)
-                  : launch_spec_demod_w<SF, MODE, false, true>(a, frames, st);
-  return a.hann ? launch_spec_demod_w<SF, MODE, true, false>(a, frames, st)
-                : launch_spec_demod_w<SF, MODE, false, false>(a, frames, st);
+  if (a.osr > 1) {
+    if (a.hann) return launch_spec_demod_w<SF, MODE, true, 0>(a, frames, st);
+    if (a.osr == 2) return launch_spec_demod_w<SF, MODE, false, 2>(a, frames, st);
+    if (a.osr == 4) return launch_spec_demod_w<SF, MODE, false, 4>(a, frames, st);
+    return launch_spec_demod_w<SF, MODE, false, 0>(a, frames, st);
+  }
+  return a.hann ? launch_spec_demod_w<SF, MODE, true, 1>(a, frames, st)
+                : launch_spec_demod_w<SF, MODE, false, 1>(a, frames, st);
 }
 
 // k_spec_fix's grid: one workgroup per CU (or fewer when the frames hold fewer data

@@ -154,7 +154,8 @@ def test_api_mode_rejects_partial_symbols(amd):
         plan.run(torch.zeros((1, 128), dtype=torch.complex64, device="cuda"))
 
 
-@pytest.mark.parametrize("sf,osr,bw", [(7, 1, 125000), (8, 2, 250000), (12, 1, 500000), (2, 3, 125000)])
+@pytest.mark.parametrize("sf,osr,bw", [(7, 1, 125000), (8, 2, 250000), (12, 1, 500000), (2, 3, 125000),
+                                       (10, 1, 125000), (11, 2, 125000), (10, 4, 250000), (12, 2, 125000)])
 def test_modulator_matches_oracle(O, amd, sf, osr, bw):
     rng = np.random.default_rng(sf + osr)
     F, S = 5, 12
@@ -164,6 +165,20 @@ def test_modulator_matches_oracle(O, amd, sf, osr, bw):
     for f in range(F):
         ref = O.lora_modulate(syms[f], sf, osr, bw, 0.9, 0x34)
         np.testing.assert_array_equal(got[f].view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("sf,frames", [(10, 2100), (12, 1030)])
+def test_modulator_many_frames_matches_oracle(O, amd, sf, frames):
+    """More than 1024 frames: k_mod_phase packs several frames per wave (ModArgs::fpw) and
+    runs the recurrence in speculative 16-step blocks; frames from the first, middle and
+    last waves against the oracle, bit for bit."""
+    rng = np.random.default_rng(sf)
+    S = 3
+    syms = rng.integers(0, 1 << sf, (frames, S)).astype(np.uint16)
+    iq = amd.modulate(torch.from_numpy(syms.astype(np.int32)).cuda(), sf, 1, 125000, 1.0, 0x12)
+    for f in (0, 1, 63, 64, frames // 2, frames - 2, frames - 1):
+        ref = O.lora_modulate(syms[f], sf, 1, 125000, 1.0, 0x12)
+        np.testing.assert_array_equal(iq[f].cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
 def test_modulator_into_a_preallocated_buffer(amd):

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""HBM traffic per kernel launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+(tools/r04_prof.sh: <dir>/pmc_fetch<tag>, <dir>/pmc_write<tag>), with the gfx950 correction
+from MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of a wide coalesced read:
+doubled).  Writes <out>.md and profiles/pmc_summary.json (read by bench.py for
+roofline.traffic): per workload the dominant kernel's HBM bytes per launch and the step's.
+
+usage: pmc_r04.py <gpurun_out/prof4> <profiles/r04/pmc_traffic.md>"""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src, dst = sys.argv[1], sys.argv[2]
+
+
+def per_kernel(d, counter):
+    acc = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        rows = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            m = re.search(r"(k_\w+(<[^>]*>)?)", r["Kernel_Name"])
+            k = m.group(1) if m else r["Kernel_Name"][:40]
+            rows[(k, r.get("Dispatch_Id", r.get("Correlation_Id", "")))] += float(r["Counter_Value"])
+        for (k, _), v in rows.items():
+            acc[k].append(v)
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+# algorithmic bytes per launch of the dominant kernel: data symbols x (8N + 2)
+# workload: (tag of the pmc_* dirs, sf, frames, data symbols, osr)
+WL = {"sf7": ("7", 7, 15625, 64, 1), "sf12": ("12", 12, 4000, 64, 1), "osr2_sf7": ("7o2", 7, 15625, 64, 2)}
+summary, lines = {}, ["# HBM traffic per launch, rocprofv3 FETCH_SIZE / WRITE_SIZE (r04)", "",
+                      "FETCH_SIZE / WRITE_SIZE in KB as reported; `read B (x2)` applies the gfx950 correction "
+                      "(MI355X_MICROARCH.md: FETCH_SIZE = half the bytes of a coalesced read).  Workloads: "
+                      "`tools/prof_workload.py` (noiseless 2 + 64-symbol frames; SF7 15,625 frames, SF12 4,000, SF7 osr 2 15,625).", "",
+                      "| workload | kernel | FETCH_SIZE KB | read B (x2) | WRITE_SIZE KB | HBM B/launch | algorithmic B | ratio |",
+                      "|---|---|---:|---:|---:|---:|---:|---:|"]
+for wl, (tag, sf, frames, S, osr) in WL.items():
+    fe = per_kernel(os.path.join(src, f"pmc_fetch{tag}"), "FETCH_SIZE")
+    wr = per_kernel(os.path.join(src, f"pmc_write{tag}"), "WRITE_SIZE")
+    N = 1 << sf
+    # the symbol pass reads every symbol's window (the sync symbols' too) and writes one
+    # u16 index per data symbol
+    algo = {"k_spec_demod": frames * ((S + 2) * 8 * N * osr + 2 * S)}
+    step = 0.0
+    d = {"step_kernels": {}}
+    for k in sorted(fe):
+        if not k.startswith(("k_spec", "k_est")):
+            continue
+        hbm = fe[k] * 1024 * 2 + wr.get(k, 0.0) * 1024
+        step += hbm
+        d["step_kernels"][k] = hbm
+        a = algo.get(k.split("<")[0])
+        lines.append(f"| {wl} | `{k}` | {fe[k]:.0f} | {fe[k] * 2048:.4g} | {wr.get(k, 0.0):.0f} | {hbm:.4g} | "
+                     f"{a if a else '-'} | {hbm / a if a else float('nan'):.4f} |")
+        if k.startswith("k_spec_demod"):
+            d.update({"kernel": k, "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": a,
+                      "traffic_over_algorithmic": hbm / a})
+    step_algo = frames * ((S + 2) * (8 * N * osr + 2) + 9)
+    d.update({"hbm_bytes_per_step": step, "algorithmic_bytes_per_step": step_algo,
+              "step_traffic_over_algorithmic": step / step_algo, "frames": frames})
+    # bench.py's workloads have 15,625 frames: the byte counts bench.py reads
+    # (hbm_bytes_per_launch / _per_step) are scaled to them; the measured ones kept as raw_*
+    scale = 15625 / frames
+    for key in ("hbm_bytes_per_launch", "hbm_bytes_per_step", "algorithmic_bytes_per_launch",
+                "algorithmic_bytes_per_step"):
+        if d.get(key) is not None:
+            d["raw_" + key] = d[key]
+            d[key] = d[key] * scale
+    summary[wl] = d
+    lines.append(f"| {wl} | whole step | | | | {step:.4g} | {step_algo:.4g} | {step / step_algo:.4f} |")
+# VALU issue of the symbol pass from the SQ passes (tools/r04_prof.sh: pmc1/pmc2 hold
+# SQ_INSTS_VALU, pmc5/pmc6 GRBM_GUI_ACTIVE for sf7/sf12): counted as 4 cycles per wave64 VALU
+# instruction (a packed fp32 instruction issues at ~0.58 of the scalar rate,
+# tools/micro/valu_rate.hip, so this under-counts a packed-heavy body); GRBM_GUI_ACTIVE sums
+# the XCDs' busy cycles.
+SIMDS, XCDS = 1024, 8
+lines += ["", "## VALU issue of the symbol pass", "",
+          "| workload | kernel | VALU wave-instr / launch | GPU cycles / launch (per XCD) | clock GHz (trace) | VALU busy |",
+          "|---|---|---:|---:|---:|---:|"]
+for wl, (_, sf, frames, S, _), (pv, pg) in zip(WL, WL.values(), (("pmc1", "pmc5"), ("pmc2", "pmc6"))):
+    vi = per_kernel(os.path.join(src, pv), "SQ_INSTS_VALU")
+    gr = per_kernel(os.path.join(src, pg), "GRBM_GUI_ACTIVE")
+    k = summary[wl].get("kernel")
+    if not k or k not in vi or k not in gr:
+        continue
+    cyc = gr[k] / XCDS
+    busy = vi[k] * 4 / (SIMDS * cyc)
+    summary[wl].update({"valu_instr_per_launch": vi[k], "gpu_cycles_per_launch": cyc, "valu_busy_frac": busy,
+                        "valu_instr_per_symbol": vi[k] / (frames * (S + 2))})
+    lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | | {busy:.3f} |")
+os.makedirs(os.path.dirname(dst), exist_ok=True)
+open(dst, "w").write("\n".join(lines) + "\n")
+json.dump(summary, open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w"), indent=1)
+print("\n".join(lines))

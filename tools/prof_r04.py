@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""Summarise a round-4 profiling call (tools/r04_prof.sh output) into markdown: per-kernel
+rocprofv3 kernel-trace statistics of each bench workload run alone (kt7: SF7 headline,
+kt7n10: SF7 at -10 dB, kt12: SF12, kt7o2: SF7 osr 2 - each run launches only that
+workload's pipeline), with each kernel's resources taken from the code-object metadata of
+the built library (tools/kernel_resources.py: VGPRs, scratch bytes per lane, static LDS),
+not from the trace; then SQ counters per launch of the pipeline kernels (pmcN passes, one
+rocprofv3 --pmc run each).
+
+usage: prof_r04.py <gpurun_out/dir> [out.md]"""
+import collections
+import csv
+import glob
+import os
+import re
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import kernel_resources  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TAGS = {"kt7": "SF7 headline (15,625 frames x 66 symbols, noiseless)",
+        "kt7n10": "SF7 at -10 dB AWGN (same shape)",
+        "kt12": "SF12 (15,625 frames x 66 symbols, noiseless)",
+        "kt7o2": "SF7 osr 2 (15,625 frames x 66 symbols, noiseless)"}
+
+
+def short(name):
+    m = re.search(r"(k_\w+(<[^>]*>)?)", name)
+    return m.group(1) if m else name[:50]
+
+
+def trace(d):
+    rows = []
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            rows.append((short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                         int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1), int(r["LDS_Block_Size"])))
+    rows.sort(key=lambda x: x[1])
+    return rows
+
+
+def main():
+    src = sys.argv[1]
+    res = {}
+    for r in kernel_resources.kernels(os.path.join(ROOT, kernel_resources.LIB)):
+        res.setdefault(short(r.get("demangled", r["name"])), r)
+    out = ["# Round-4 kernel statistics (rocprofv3 --kernel-trace --stats)", "",
+           "Each workload alone (`tools/prof_workload.py`, eager `plan.run` per step).  Resources: code-object "
+           "metadata of the built `liblora_mi355x.so` (`tools/kernel_resources.py`); `LDS B (launch)` is the "
+           "trace's allocation for the launch (static + dynamic).  The tracer serialises dispatches; bench.py's "
+           "HIP-event stage times are measured without it.", ""]
+    for tag, what in TAGS.items():
+        rows = trace(os.path.join(src, tag))
+        if not rows:
+            continue
+        agg = collections.OrderedDict()
+        for k, b, e, wg, lds in rows:
+            a = agg.setdefault((k, wg), {"n": 0, "ns": [], "lds": lds})
+            a["n"] += 1
+            a["ns"].append(e - b)
+        out += [f"## {tag}: {what}", "",
+                "| kernel | workgroups | launches | avg us | min us | max us | LDS B (launch) | VGPR | AGPR | "
+                "scratch B/lane | VGPR spills |",
+                "|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
+        for (k, wg), a in sorted(agg.items(), key=lambda kv: -sum(kv[1]["ns"])):
+            if not k.startswith("k_"):
+                continue
+            r = res.get(k, {})
+            ns = a["ns"]
+            out.append(f"| `{k}` | {wg} | {a['n']} | {sum(ns) / len(ns) / 1e3:.2f} | {min(ns) / 1e3:.2f} | "
+                       f"{max(ns) / 1e3:.2f} | {a['lds']} | {r.get('vgpr_count', '?')} | {r.get('agpr_count', '?')} | "
+                       f"{r.get('private_segment_fixed_size', '?')} | {r.get('vgpr_spill_count', '?')} |")
+        pipe = [r for r in rows if r[0].startswith(("k_est", "k_cert", "k_spec"))]
+        gaps = sorted(pipe[i + 1][1] - pipe[i][2] for i in range(len(pipe) - 1))
+        if gaps:
+            out += ["", f"gap between consecutive pipeline kernels under the tracer: median "
+                        f"{gaps[len(gaps) // 2] / 1e3:.1f} us", ""]
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    cnt = collections.defaultdict(lambda: collections.defaultdict(int))
+    for f in sorted(glob.glob(os.path.join(src, "pmc[0-9]*", "**", "*counter_collection.csv"), recursive=True)):
+        seen = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k.startswith("k_"):
+                seen[(k, r["Counter_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
+        for (k, n, _), v in seen.items():
+            per[k][n] += v
+            cnt[k][n] += 1
+    if per:
+        out += ["## SQ counters per launch (summed over XCDs / SEs, averaged over launches)", "",
+                "SF7 workloads: 15,625 frames; SF12: 4,000 frames (tools/r04_prof.sh).", ""]
+        for k in sorted(per):
+            if not k.startswith(("k_spec_demod", "k_est", "k_cert")):
+                continue
+            c = {n: per[k][n] / max(cnt[k][n], 1) for n in per[k]}
+            out += [f"### `{k}`", "", "| counter | per launch |", "|---|---:|"]
+            out += [f"| {n} | {c[n]:.4g} |" for n in sorted(c)]
+            wc = c.get("SQ_WAVE_CYCLES")
+            if wc:
+                for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                          "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_VMEM"):
+                    if n in c:
+                        out.append(f"| {n} / SQ_WAVE_CYCLES | {c[n] / wc:.3f} |")
+            if c.get("SQ_INSTS_LDS"):
+                out.append(f"| SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS | {c.get('SQ_LDS_BANK_CONFLICT', 0) / c['SQ_INSTS_LDS']:.3f} |")
+            if c.get("SQ_WAVES"):
+                for n in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VALU_TRANS_F32"):
+                    if n in c:
+                        out.append(f"| {n} per wave | {c[n] / c['SQ_WAVES']:.1f} |")
+            out.append("")
+    text = "\n".join(out) + "\n"
+    if len(sys.argv) > 2:
+        open(sys.argv[2], "w").write(text)
+    print(text)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One bench workload alone, for a profiler: the pipeline over `frames` frames of 2 + 64
 symbols (bench.py's make_input: GPU modulation, optional AWGN at `snr` dB), `steps`
-times.  usage: prof_workload.py <sf> [snr_db|none] [frames] [steps] [data_symbols]"""
+times.  usage: prof_workload.py <sf> [snr_db|none] [frames] [steps] [data_symbols] [osr]"""
 import os
 import sys
 
@@ -18,9 +18,10 @@ snr = None if len(sys.argv) < 3 or sys.argv[2] == "none" else float(sys.argv[2])
 frames = int(sys.argv[3]) if len(sys.argv) > 3 else 15625
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 data_syms = int(sys.argv[5]) if len(sys.argv) > 5 else 64
+osr = int(sys.argv[6]) if len(sys.argv) > 6 else 1
 dev = torch.device("cuda", 0)
-_, iq = bench.make_input(sf, frames, data_syms, 20251015, dev, snr)
-plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=dev)
+_, iq = bench.make_input(sf, frames, data_syms, 20251015, dev, snr, osr=osr)
+plan = amd.DemodPlan(sf, osr, 125000, "none", dechirp=True, mode="legacy", device=dev)
 out = None
 for _ in range(steps):
     out = plan.run(iq, out)
