@@ -73,31 +73,52 @@ constexpr int leaf_pos(int R, int v) {
   return pos;
 }
 
-// LDS image of DIT position p: slot(p) = p + sum_{i>=0} bit_{4+i}(p) * W[i].  The
-// weights (and the row pad) were searched with tools/lds/lds_search_add.py against the
+// LDS image of DIT position p: slot(p) = p + bit_3(p) * W3 + sum_{i>=0} bit_{4+i}(p) * W[i].
+// The weights (and the row pad) were searched with tools/lds/lds_search_add.py against the
 // MI355X banking rules (ds_read_b64: 2 x 32 lanes, 64 banks; ds_write_b64: 4 x 16
 // lanes, 32 banks) over every access of the transform - pass-1 write-back, LDS-pass
 // reads and write-backs, natural-order write: mean conflict degree 1.0-1.4 (the
 // former p + p/R1 map reached 2-5.5, 16-way on the SF11/12 pass-1 write-back).  The
 // search keeps every weight >= the sum of the lower ones (injective, asserted below).
+// W3 (bit 3, default 0): SF7's pass-1 write-back puts a lane's two 8-position blocks
+// (positions c 8 + u, c = rev[l] >> 3) 8 slots apart, which no map over bits >= 4 can
+// separate from the neighbouring symbol's row (rowc = 8 mod 16, what the pass-A reads
+// need): 2-way on every write (SQ_LDS_BANK_CONFLICT 1.9 per LDS instruction of the SF7
+// symbol pass).  W3 = 1 with W = {1, 2, 4} (tools/lds/lds_search_bit3.py) is conflict-free
+// on the write-back, the pass-A reads (ds_read_b64 and ds_read2_b64) and the
+// natural-order write, at the same row length.
 // Being linear in the bits of p, slot(base | off) = slot(base) + slot(off) when base and
 // off use disjoint bits: every access splits into a per-lane part and a compile-time
 // part that folds into the ds_* immediate offset.
 template <int SF>
 struct LdsMap;
 template <> struct LdsMap<6> { static constexpr int W[2] = {1, 2}; static constexpr int PAD = 1; };
-template <> struct LdsMap<7> { static constexpr int W[3] = {1, 3, 4}; static constexpr int PAD = 0; };
+template <> struct LdsMap<7> {
+  static constexpr int W3 = 1;
+  static constexpr int W[3] = {1, 2, 4};
+  static constexpr int PAD = 0;
+};
 template <> struct LdsMap<8> { static constexpr int W[4] = {1, 2, 4, 8}; static constexpr int PAD = 1; };
 template <> struct LdsMap<9> { static constexpr int W[5] = {0, 1, 4, 8, 14}; static constexpr int PAD = 0; };
 template <> struct LdsMap<10> { static constexpr int W[6] = {0, 0, 1, 2, 4, 8}; static constexpr int PAD = 0; };
 template <> struct LdsMap<11> { static constexpr int W[7] = {0, 0, 2, 8, 10, 20, 43}; static constexpr int PAD = 0; };
 template <> struct LdsMap<12> { static constexpr int W[8] = {0, 0, 0, 0, 1, 2, 4, 8}; static constexpr int PAD = 0; };
 
-// Injectivity: each weight is at least the sum of the lower ones, so the offset of a
-// 16-position block is monotone in the block index and blocks never overlap.
+// bit 3's weight: LdsMap<SF>::W3 where declared, else 0
+template <int SF, class = void>
+struct LdsW3 {
+  static constexpr int v = 0;
+};
+template <int SF>
+struct LdsW3<SF, std::void_t<decltype(LdsMap<SF>::W3)>> {
+  static constexpr int v = LdsMap<SF>::W3;
+};
+
+// Injectivity: each weight (W3 the lowest) is at least the sum of the lower ones, so
+// slot(p) is strictly increasing in p and blocks never overlap.
 template <int SF>
 constexpr bool lds_map_injective() {
-  int acc = 0;
+  int acc = LdsW3<SF>::v;
   for (int i = 0; i < SF - 4; ++i) {
     if (LdsMap<SF>::W[i] < acc) return false;
     acc += LdsMap<SF>::W[i];
@@ -114,7 +135,7 @@ __host__ __device__ constexpr int lds_slot(int p) {
   if constexpr (SF <= 5) {
     return p;
   } else {
-    int s = p;
+    int s = p + ((p >> 3) & 1) * LdsW3<SF>::v;
     for (int i = 0; i < SF - 4; ++i) s += ((p >> (4 + i)) & 1) * LdsMap<SF>::W[i];
     return s;
   }
@@ -125,7 +146,7 @@ constexpr int lds_row() {  // complex elements per symbol row
   if constexpr (SF <= 5) {
     return 1 << SF;
   } else {
-    int w = 0;
+    int w = LdsW3<SF>::v;
     for (int i = 0; i < SF - 4; ++i) w += LdsMap<SF>::W[i];
     return (1 << SF) + w + LdsMap<SF>::PAD;
   }
