@@ -68,25 +68,37 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2f pk(cf a) { return __builtin_bit_cast(v2f, a); }
 __device__ __forceinline__ cf unpk(v2f a) { return __builtin_bit_cast(cf, a); }
 // a * w with the reference's roundings: (fl(ar wr) - fl(ai wi), fl(ai wr) + fl(ar wi)) = cmul
+// Each helper's dependent instructions sit in ONE asm statement: the hazard recognizer
+// cannot see inside an inline asm, so it pads every asm that reads a VGPR the previous asm
+// just wrote with an s_nop - one per complex product when each instruction was its own
+// statement (110 s_nops per symbol in the SF12 symbol pass's loop).  Back to back, the
+// hardware interlocks these VALU -> VALU dependences itself (the compiler's own packed code
+// carries no wait states there).  "=&v": the result is written before the last input read.
 __device__ __forceinline__ cf pk_cmul_ref(cf a, cf w) {
   v2f p, q, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(p) : "v"(pk(a)), "v"(pk(w)));          // (ar wr, ai wr)
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1]" : "=v"(q) : "v"(pk(a)), "v"(pk(w)));             // (ar wi, ai wi)
-  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(p), "v"(q));
+  asm("v_pk_mul_f32 %1, %3, %4 op_sel_hi:[1,0]\n\t"                                   // (ar wr, ai wr)
+      "v_pk_mul_f32 %2, %3, %4 op_sel:[0,1]\n\t"                                      // (ar wi, ai wi)
+      "v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]"
+      : "=v"(r), "=&v"(p), "=&v"(q)
+      : "v"(pk(a)), "v"(pk(w)));
   return unpk(r);
 }
 // a * w: (fma(-ai, wi, fl(ar wr)), fma(ar, wi, fl(ai wr)))
 __device__ __forceinline__ v2f pk_cmul(v2f a, v2f w) {
   v2f t, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(w));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[1,0]\n\t"
+      "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+      : "=v"(r), "=&v"(t)
+      : "v"(a), "v"(w));
   return r;
 }
 // c + a * w: (fma(-ai, wi, fma(ar, wr, cr)), fma(ar, wi, fma(ai, wr, ci)))
 __device__ __forceinline__ v2f pk_cfma(v2f a, v2f w, v2f c) {
   v2f t, r;
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(a), "v"(w), "v"(c));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  asm("v_pk_fma_f32 %1, %2, %3, %4 op_sel_hi:[1,0,1]\n\t"
+      "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+      : "=v"(r), "=&v"(t)
+      : "v"(a), "v"(w), "v"(c));
   return r;
 }
 __device__ __forceinline__ v2f pk_add(v2f a, v2f b) {
@@ -146,15 +158,29 @@ __device__ __forceinline__ cf cscale(cf a, float s) { return {a.re * s, a.im * s
 template <bool FMA = false>
 __device__ __forceinline__ void bfly4(cf& f0, cf& f1, cf& f2, cf& f3, cf w1, cf w2, cf w3) {
   if constexpr (FMA) {
-    const v2f A = pk_cfma(pk(f2), pk(w2), pk(f0));
-    const v2f B = pk_twice_minus(pk(f0), A);
-    const v2f P = pk_cmul(pk(f3), pk(w3));
-    const v2f C = pk_cfma(pk(f1), pk(w1), P);
-    const v2f D = pk_minus_twice(C, P);
-    f0 = unpk(pk_add(A, C));
-    f2 = unpk(pk_sub(A, C));
-    f1 = unpk(pk_sub_j(B, D));
-    f3 = unpk(pk_add_j(B, D));
+    // pk_cfma(f2, w2, f0) = A, pk_cmul(f3, w3) = P, pk_twice_minus(f0, A) = B,
+    // pk_cfma(f1, w1, P) = C, pk_minus_twice(C, P) = D, then pk_add / pk_sub / pk_sub_j /
+    // pk_add_j - the same twelve instructions, in one asm statement (no hazard padding
+    // between them; see pk_cmul_ref), the two products' halves interleaved
+    v2f x0 = pk(f0), x1 = pk(f1), x2 = pk(f2), x3 = pk(f3), A, B, P, C, D;
+    asm("v_pk_fma_f32 %4, %2, %9, %0 op_sel_hi:[1,0,1]\n\t"
+        "v_pk_mul_f32 %6, %3, %10 op_sel_hi:[1,0]\n\t"
+        "v_pk_fma_f32 %4, %2, %9, %4 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\t"
+        "v_pk_fma_f32 %6, %3, %10, %6 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\t"
+        "v_pk_fma_f32 %7, %1, %11, %6 op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %5, %0, 2.0, %4 op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]\n\t"
+        "v_pk_fma_f32 %7, %1, %11, %7 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\t"
+        "v_pk_fma_f32 %8, %6, -2.0, %7 op_sel_hi:[1,0,1]\n\t"
+        "v_pk_add_f32 %0, %4, %7\n\t"
+        "v_pk_add_f32 %2, %4, %7 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %1, %5, %8 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %3, %5, %8 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]"
+        : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=&v"(A), "=&v"(B), "=&v"(P), "=&v"(C), "=&v"(D)
+        : "v"(pk(w2)), "v"(pk(w3)), "v"(pk(w1)));
+    f0 = unpk(x0);
+    f1 = unpk(x1);
+    f2 = unpk(x2);
+    f3 = unpk(x3);
     return;
   }
   const cf s0 = cmul_t<FMA>(f1, w1);
@@ -177,12 +203,22 @@ __device__ __forceinline__ void bfly4(cf& f0, cf& f1, cf& f2, cf& f3, cf w1, cf 
 template <bool PK = false>
 __device__ __forceinline__ void bfly4_unit(cf& f0, cf& f1, cf& f2, cf& f3) {
   if constexpr (PK) {
-    const v2f s5 = pk_sub(pk(f0), pk(f2)), a0 = pk_add(pk(f0), pk(f2));
-    const v2f s3 = pk_add(pk(f1), pk(f3)), s4 = pk_sub(pk(f1), pk(f3));
-    f2 = unpk(pk_sub(a0, s3));
-    f0 = unpk(pk_add(a0, s3));
-    f1 = unpk(pk_sub_j(s5, s4));  // s5 + (s4.im, -s4.re)
-    f3 = unpk(pk_add_j(s5, s4));
+    // s5 = f0 - f2, a0 = f0 + f2, s3 = f1 + f3, s4 = f1 - f3; f2 = a0 - s3, f0 = a0 + s3,
+    // f1 = s5 - j s4 = s5 + (s4.im, -s4.re), f3 = s5 + j s4 (one asm statement, as bfly4)
+    v2f x0 = pk(f0), x1 = pk(f1), x2 = pk(f2), x3 = pk(f3), s5, a0, s3, s4;
+    asm("v_pk_add_f32 %4, %0, %2 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %5, %0, %2\n\t"
+        "v_pk_add_f32 %6, %1, %3\n\t"
+        "v_pk_add_f32 %7, %1, %3 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %2, %5, %6 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %0, %5, %6\n\t"
+        "v_pk_add_f32 %1, %4, %7 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %3, %4, %7 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]"
+        : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=&v"(s5), "=&v"(a0), "=&v"(s3), "=&v"(s4));
+    f0 = unpk(x0);
+    f1 = unpk(x1);
+    f2 = unpk(x2);
+    f3 = unpk(x3);
     return;
   }
   const cf s5 = csub(f0, f2);
@@ -213,9 +249,14 @@ __device__ __forceinline__ void bfly2_unit(cf& f0, cf& f1) {
 // kissfft.hh:155-162 kf_bfly2 (forward).
 template <bool FMA = false>
 __device__ __forceinline__ void bfly2(cf& f0, cf& f1, cf w) {
-  if constexpr (FMA) {  // A = f0 + w f1, B = 2 f0 - A: 3 packed operations
-    const v2f A = pk_cfma(pk(f1), pk(w), pk(f0));
-    f1 = unpk(pk_twice_minus(pk(f0), A));
+  if constexpr (FMA) {  // A = f0 + w f1 (pk_cfma), B = 2 f0 - A (pk_twice_minus): one asm
+    v2f x0 = pk(f0), x1 = pk(f1), A;
+    asm("v_pk_fma_f32 %2, %1, %3, %0 op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %2, %1, %3, %2 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\t"
+        "v_pk_fma_f32 %1, %0, 2.0, %2 op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]"
+        : "+v"(x0), "+v"(x1), "=&v"(A)
+        : "v"(pk(w)));
+    f1 = unpk(x1);
     f0 = unpk(A);
     return;
   }
