@@ -1604,8 +1604,21 @@ __device__ __forceinline__ void certify_list(const KArgs& a, int64_t f, const Fr
   }
 }
 
+// SF 10-12: the pre-pass's transforms are the certified kind (fused multiply-adds, constant
+// pass-1 twiddles, no exact-arithmetic temporaries), so its estimate qs is close to, not
+// identical with, the reference's; stage 2 then estimates EVERY frame exactly (scaled or
+// not) and the certification's |r - r'| N term and t_off check carry the difference.
+constexpr bool est_prepass_approx(int SF, int SPEC) { return SPEC == 1 && SF >= 10; }
+// waves per SIMD the estimate kernels' registers are budgeted for
+// (SF 10-12, same-box A/B: the pre-pass at 3 waves (148 VGPRs, no spill) and stage 2 at 4
+// (128; SF11 at 3, where 4 spilled) - the SF12 estimate stages at -10 dB 1.17 -> 0.84 ms,
+// noiseless even; 4 waves for the pre-pass spilled 10 VGPRs for no gain)
+constexpr int est_waves_per_eu(int SF, int SPEC) {
+  return est_prepass_approx(SF, SPEC) ? 3 : (SPEC == 2 && SF >= 10) ? (SF == 11 ? 3 : 4) : 2;
+}
+
 template <int SF, int MODE, int SPEC = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(est_waves_per_eu(SF, SPEC))))
 k_est_fast(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
@@ -1649,7 +1662,9 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
   }
   const int scaled = maxv > 1.0f;
   const float scale = scaled ? 1.0f / maxv : 1.0f;
-  if constexpr (SPEC == 2) {
+  // an unscaled frame's pre-pass estimate is the reference's when the pre-pass was exact
+  constexpr bool TAKE_PRE = SPEC == 2 && !est_prepass_approx(SF, 1);
+  if constexpr (TAKE_PRE) {
     // max <= 1: no rescaling, so the pre-pass estimate and its sync word are already the
     // reference's (identical inputs and arithmetic); the symbols, rotated with the
     // hardware sine/cosine, go through the certification below like a rescaled frame's.
@@ -1666,7 +1681,7 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
   // The frame's exact offsets: estimated below, or for an unscaled frame of the
   // speculative pipeline the pre-pass's (identical), whose symbols are then certified.
   FrameParams q;
-  if (SPEC == 2 && !scaled) {
+  if (TAKE_PRE && !scaled) {
     q = a.fp_spec[f];
   } else {
 
@@ -1743,15 +1758,21 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
       unsigned best_t = 0;
       cf best_bin = {0.0f, 0.0f};
       for (int t = 0; t < osr; ++t) {
-        gather_points<SF>(a, x + (int64_t)s * step + t, l, osr, step, t, legacy ? 1 : 0, dech,
+        // the lane index opaque per transform: left visible, the compiler hoists the lane's
+        // 64-bit sample, table and twiddle addresses of both symbols out of the loops and
+        // keeps them live across the transforms (SF12 pre-pass: 147 VGPRs of spills under
+        // the 4-wave budget)
+        int lo = l;
+        asm volatile("" : "+v"(lo));
+        gather_points<SF>(a, x + (int64_t)s * step + t, lo, osr, step, t, legacy ? 1 : 0, dech,
                              scale, in);
         if constexpr (SPEC == 1) {
 #pragma unroll
           for (int q = 0; q < P; ++q) mo = amax3(mo, in[q]);
           asm volatile("" : "+v"(mo));
         }
-        rotate_place<SF, false>(in, z, 0.0f, 0.0f, hann, a.win, l);
-        uint64_t key = fft_key<SF, true>(z, row, l, a);
+        rotate_place<SF, false>(in, z, 0.0f, 0.0f, hann, a.win, lo);
+        uint64_t key = fft_key<SF, true, est_prepass_approx(SF, SPEC)>(z, row, lo, a);
         key = symbol_key<SF>(key, tid, red);
         if (l == 0) {
           const uint32_t idx = key_index(key);
@@ -1975,12 +1996,15 @@ k_spec_fix(KArgs a, int rowc, int64_t grid) {
     const bool sync = j == 0xFFFFFFFFu;  // the sync word: symbols 0 and 1
     const FrameParams q = a.fp[f];
     const cf* __restrict__ x = a.iq + f * a.frame_stride;
-    const uint32_t i0 = exact_symbol<SF, MODE>(a, x, q, sync ? 0 : 2 + (int)j, row, l, tid, red);
+    // the lane index opaque per entry (k_est_fast: no lane addresses hoisted out of the loop)
+    int lo = l;
+    asm volatile("" : "+v"(lo));
+    const uint32_t i0 = exact_symbol<SF, MODE>(a, x, q, sync ? 0 : 2 + (int)j, row, lo, tid, red);
     // a second transform when any group of the workgroup holds a sync entry (uniform, so
     // the transform's barriers match); the others repeat theirs
     const bool any_sync = G::WAVE_LOCAL ? __any(sync) : __syncthreads_or(sync);
     uint32_t i1 = 0;
-    if (any_sync) i1 = exact_symbol<SF, MODE>(a, x, q, sync ? 1 : 2 + (int)j, row, l, tid, red);
+    if (any_sync) i1 = exact_symbol<SF, MODE>(a, x, q, sync ? 1 : 2 + (int)j, row, lo, tid, red);
     if (l == 0 && valid) {
       if (!sync) {
         if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)i0;
