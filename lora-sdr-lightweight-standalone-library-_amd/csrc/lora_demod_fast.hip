@@ -1604,21 +1604,22 @@ __device__ __forceinline__ void certify_list(const KArgs& a, int64_t f, const Fr
   }
 }
 
-// SF 10-12: the pre-pass's transforms are the certified kind (fused multiply-adds, constant
-// pass-1 twiddles, no exact-arithmetic temporaries), so its estimate qs is close to, not
-// identical with, the reference's; stage 2 then estimates EVERY frame exactly (scaled or
-// not) and the certification's |r - r'| N term and t_off check carry the difference.
-constexpr bool est_prepass_approx(int SF, int SPEC) { return SPEC == 1 && SF >= 10; }
-// waves per SIMD the estimate kernels' registers are budgeted for
-// (SF 10-12, same-box A/B: the pre-pass at 3 waves (148 VGPRs, no spill) and stage 2 at 4
-// (128; SF11 at 3, where 4 spilled) - the SF12 estimate stages at -10 dB 1.17 -> 0.84 ms,
-// noiseless even; 4 waves for the pre-pass spilled 10 VGPRs for no gain)
-constexpr int est_waves_per_eu(int SF, int SPEC) {
-  return est_prepass_approx(SF, SPEC) ? 3 : (SPEC == 2 && SF >= 10) ? (SF == 11 ? 3 : 4) : 2;
+// Waves per SIMD the estimate kernels' registers are budgeted for.  SF 10-12 (T >= 64 lanes
+// per frame): the pipeline's pre-pass and stage 2 at 4 (osr > 1 pre-pass and SF11 stage 2
+// at 3, where 4 spilled) - with the lane index opaque per transform they fit; before, the
+// hoisted lane addresses took 256 VGPRs and held them at 2.  Tried and not kept: the
+// pre-pass with the certified (FMA) transforms, its estimate only steering the symbol pass
+// and stage 2 estimating every frame exactly - even for rescaled frames, and 0.34 ms slower
+// per SF12 step for unscaled ones, whose exact pre-pass estimate stage 2 takes as it is.
+constexpr int est_waves_per_eu(int SF, int MODE, int SPEC) {
+  if (SF < 10) return 2;
+  if (SPEC == 1) return MODE == 2 ? 3 : 4;
+  if (SPEC == 2) return SF == 11 ? 3 : 4;
+  return 2;
 }
 
 template <int SF, int MODE, int SPEC = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(est_waves_per_eu(SF, SPEC))))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(est_waves_per_eu(SF, MODE, SPEC))))
 k_est_fast(KArgs a, int64_t frames, int rowc) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P;
@@ -1662,9 +1663,7 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
   }
   const int scaled = maxv > 1.0f;
   const float scale = scaled ? 1.0f / maxv : 1.0f;
-  // an unscaled frame's pre-pass estimate is the reference's when the pre-pass was exact
-  constexpr bool TAKE_PRE = SPEC == 2 && !est_prepass_approx(SF, 1);
-  if constexpr (TAKE_PRE) {
+  if constexpr (SPEC == 2) {
     // max <= 1: no rescaling, so the pre-pass estimate and its sync word are already the
     // reference's (identical inputs and arithmetic); the symbols, rotated with the
     // hardware sine/cosine, go through the certification below like a rescaled frame's.
@@ -1681,7 +1680,7 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
   // The frame's exact offsets: estimated below, or for an unscaled frame of the
   // speculative pipeline the pre-pass's (identical), whose symbols are then certified.
   FrameParams q;
-  if (TAKE_PRE && !scaled) {
+  if (SPEC == 2 && !scaled) {
     q = a.fp_spec[f];
   } else {
 
@@ -1760,8 +1759,8 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
       for (int t = 0; t < osr; ++t) {
         // the lane index opaque per transform: left visible, the compiler hoists the lane's
         // 64-bit sample, table and twiddle addresses of both symbols out of the loops and
-        // keeps them live across the transforms (SF12 pre-pass: 147 VGPRs of spills under
-        // the 4-wave budget)
+        // keeps them live across the transforms (SF12: 256 VGPRs with spills at a 2-wave
+        // budget, 147 VGPRs of spills at 4)
         int lo = l;
         asm volatile("" : "+v"(lo));
         gather_points<SF>(a, x + (int64_t)s * step + t, lo, osr, step, t, legacy ? 1 : 0, dech,
@@ -1772,7 +1771,7 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
           asm volatile("" : "+v"(mo));
         }
         rotate_place<SF, false>(in, z, 0.0f, 0.0f, hann, a.win, lo);
-        uint64_t key = fft_key<SF, true, est_prepass_approx(SF, SPEC)>(z, row, lo, a);
+        uint64_t key = fft_key<SF, true>(z, row, lo, a);
         key = symbol_key<SF>(key, tid, red);
         if (l == 0) {
           const uint32_t idx = key_index(key);
