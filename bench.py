@@ -513,11 +513,14 @@ def roofline(r, probe=None):
             "traffic": pmc_dom,
             "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch, "
                               "tools/pmc_r04.py; committed, not measured in this run)",
-            # the kernel's other roof: VALU issue (SQ_INSTS_VALU x 4 cycles over 1024 SIMDs x the
+            # the kernel's other roof: VALU issue (SQ_INSTS_VALU x its issue cycles - 4 per
+            # instruction, packed ones weighted by their 0.58 issue rate - over 1024 SIMDs x the
             # GRBM-measured cycles of the same launch, committed profile)
             "valu": {"busy_frac": load_pmc(wl, "valu_busy_frac"),
+                     "busy_frac_4cycle": load_pmc(wl, "valu_busy_frac_4cycle"),
                      "instr_per_symbol": load_pmc(wl, "valu_instr_per_symbol"),
-                     "source": "profiles/pmc_summary.json (rocprofv3 SQ_INSTS_VALU, GRBM_GUI_ACTIVE)"},
+                     "source": "profiles/pmc_summary.json (rocprofv3 SQ_INSTS_VALU, GRBM_GUI_ACTIVE; "
+                               "tools/pmc_r04.py)"},
             "pipeline": {"algorithmic_bytes_per_step": r["step_bytes"], "ms_per_step": r["ms_per_step"],
                          "achieved": r["pipeline_gbs"], "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS,
                          "counter_bytes_per_step": pmc_step,

@@ -82,8 +82,14 @@ for wl, (tag, sf, frames, S, osr) in WL.items():
 # tools/micro/valu_rate.hip, so this under-counts a packed-heavy body); GRBM_GUI_ACTIVE sums
 # the XCDs' busy cycles.
 SIMDS, XCDS = 1024, 8
+# Share of packed (v_pk_*) instructions among the VALU instructions of the symbol pass's
+# steady-state loop (static counts from the disassembly of the built kernels: SF7 262 of
+# 505, SF12 378 of 639) and a packed instruction's issue cost in 4-cycle slots (it issues at
+# ~0.58 of the scalar rate, tools/micro/valu_rate.hip): the issue-weighted busy fraction.
+PK_SHARE = {"sf7": 262 / 505, "sf12": 378 / 639}
+PK_COST = 1 / 0.58
 lines += ["", "## VALU issue of the symbol pass", "",
-          "| workload | kernel | VALU wave-instr / launch | GPU cycles / launch (per XCD) | clock GHz (trace) | VALU busy |",
+          "| workload | kernel | VALU wave-instr / launch | GPU cycles / launch (per XCD) | VALU busy (4 cycles each) | VALU busy (packed weighted) |",
           "|---|---|---:|---:|---:|---:|"]
 for wl, (_, sf, frames, S, _), (pv, pg) in zip(WL, WL.values(), (("pmc1", "pmc5"), ("pmc2", "pmc6"))):
     vi = per_kernel(os.path.join(src, pv), "SQ_INSTS_VALU")
@@ -92,10 +98,13 @@ for wl, (_, sf, frames, S, _), (pv, pg) in zip(WL, WL.values(), (("pmc1", "pmc5"
     if not k or k not in vi or k not in gr:
         continue
     cyc = gr[k] / XCDS
-    busy = vi[k] * 4 / (SIMDS * cyc)
+    busy4 = vi[k] * 4 / (SIMDS * cyc)
+    w = PK_SHARE[wl] * PK_COST + (1 - PK_SHARE[wl])
+    busy = busy4 * w
     summary[wl].update({"valu_instr_per_launch": vi[k], "gpu_cycles_per_launch": cyc, "valu_busy_frac": busy,
+                        "valu_busy_frac_4cycle": busy4, "valu_packed_share": PK_SHARE[wl],
                         "valu_instr_per_symbol": vi[k] / (frames * (S + 2))})
-    lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | | {busy:.3f} |")
+    lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | {busy4:.3f} | {busy:.3f} |")
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 open(dst, "w").write("\n".join(lines) + "\n")
 json.dump(summary, open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w"), indent=1)

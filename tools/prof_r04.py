@@ -76,6 +76,28 @@ def main():
         if gaps:
             out += ["", f"gap between consecutive pipeline kernels under the tracer: median "
                         f"{gaps[len(gaps) // 2] / 1e3:.1f} us", ""]
+    # bench.py itself under the tracer: its HIP-event stage times beside rocprofv3's averages
+    import json
+    for tag, key in (("bench7", None), ("bench12", "sf12")):
+        rows = trace(os.path.join(src, tag))
+        jf = os.path.join(src, tag + ".json")
+        if not rows or not os.path.exists(jf):
+            continue
+        d = json.loads(open(jf).read().strip().splitlines()[-1])
+        r = d if key is None else d
+        stage = r["config"]["stage_ms"] if key is None else r["stage_ms"]
+        agg = collections.defaultdict(list)
+        for k, b, e, wg, lds in rows:
+            if k.startswith(("k_spec", "k_est", "k_cert")):
+                agg[k].append(e - b)
+        out += [f"## {tag}: `python bench.py {'--no-cpu --no-channels --no-fast --no-variants --no-sf12' if key is None else '--sf12-only'}` under rocprofv3 --kernel-trace --stats", "",
+                f"bench.py's HIP-event stage times in the same run (ms per step): estimate stages {stage[1]:.4f}, "
+                f"symbol pass {stage[2]:.4f}; ms_per_step {r['ms_per_step']:.4f} (timed steps replay a HIP graph; "
+                f"the tracer serialises them)", "",
+                "| kernel | launches | avg us (rocprofv3) |", "|---|---:|---:|"]
+        for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+            out.append(f"| `{k}` | {len(v)} | {sum(v) / len(v) / 1e3:.2f} |")
+        out.append("")
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     cnt = collections.defaultdict(lambda: collections.defaultdict(int))
     for f in sorted(glob.glob(os.path.join(src, "pmc[0-9]*", "**", "*counter_collection.csv"), recursive=True)):

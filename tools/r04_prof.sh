@@ -32,4 +32,10 @@ for cfg in "7:7 none 15625 2" "12:12 none 4000 2" "7o2:7 none 15625 2 64 2"; do
     timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$t$tag -o run -- python3 tools/prof_workload.py $args > $OUT/pmc_$t$tag.log 2>&1 || { echo "$c pass failed"; tail -3 $OUT/pmc_$t$tag.log; exit 2; }
   done
 done
+# the bench's own headline and SF12 lines under the tracer (the same command's HIP-event
+# stage times next to rocprofv3's per-kernel averages)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench7 -o run -- \
+  python3 bench.py --no-cpu --no-channels --no-fast --no-variants --no-sf12 > $OUT/bench7.json 2> $OUT/bench7.err || { tail -5 $OUT/bench7.err; exit 2; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench12 -o run -- \
+  python3 bench.py --sf12-only > $OUT/bench12.json 2> $OUT/bench12.err || { tail -5 $OUT/bench12.err; exit 2; }
 echo "== done $(date +%T)"
