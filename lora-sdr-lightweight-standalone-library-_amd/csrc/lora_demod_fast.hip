@@ -1125,13 +1125,16 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
     float4 dt[MODE == 0 ? P / 2 : 1];
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
     const int vt = (cg + lr) * 16;
+    // data windows are read once (nontemporal); the sync symbols, the grid's last blocks, with
+    // the default policy: stage 2 re-reads symbols 0/1 right after this pass
+    constexpr int AUX = SYNC ? 0 : 2;
 #pragma unroll
     for (int pp = 0; pp < P / 2; ++pp) {
       if constexpr (MODE == 0)
         dt[pp] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vt, pp * (N + T) * 16, 0));
 #pragma unroll
       for (int q = 2 * pp; q < 2 * pp + 2; ++q)
-        ld[q] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
+        ld[q] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, AUX));
     }
     // (only waves holding a lane l < d: for T > 64 the symbol's first wave)
     if (AL && __builtin_amdgcn_readfirstlane(__ballot(l < d) != 0)) {
@@ -1139,7 +1142,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       // to T samples past the window, possibly past the batch) re-read load 15's sample
       const bool late = l < d;
       ld[P] = __builtin_bit_cast(
-          v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, late ? vo : vo - T * 8, P * T * 8, 2 /* nt */));
+          v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, late ? vo : vo - T * 8, P * T * 8, AUX));
 #pragma unroll
       for (int q = 0; q < P; ++q) ld[q] = late ? ld[q + 1] : ld[q];  // ascending: ld[q + 1] not yet moved
     }
