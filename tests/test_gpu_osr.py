@@ -5,7 +5,7 @@ of the frame and an offset estimate over the osr phases of symbols 0/1
 (/root/reference/src/phy/LoRaDemod.cpp:59-77, 86-111, 141-162); its only real-capture
 fixture is osr 2 (tests/gr_lora_sdr_interop.cpp:34).  Here each frame is read once: the
 symbol pass transforms every osr-th sample of a window and takes the window's maximum over
-all of them (k_spec_demod<..., OSRN>), the pre-pass / stage 2 estimate over the osr phases
+all of them (k_spec_demod<..., OSRV>: osr 2 / 4 in 16-byte loads, 3 and Hann at run-time osr), the pre-pass / stage 2 estimate over the osr phases
 (k_est_fast<SF, 2, 1|2>), rejected symbols recomputed exactly (k_spec_fix<SF, 2>).  Every
 output is compared with the oracle bit for bit, and the plan must report the pipeline."""
 import numpy as np
