@@ -187,10 +187,15 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 // for the sign of a zero component, and a zero's sign never reaches a non-zero result
 // or |X|^2, so every bin magnitude - hence the argmax - is bit-identical.  Transforms
 // whose bin values are used (the estimate's phase) keep the multiplies.
-template <int R, bool R2, int N, int MA, bool UNIT = false, bool FMA = false, class TWP = const cf*>
+// SKIP1: the first stage (the radix-2 one, or the first radix-4 one) was already done by the
+// caller (the certified symbol pass folds its rotation factors into it, fft_key FOLD).
+template <int R, bool R2, int N, int MA, bool UNIT = false, bool FMA = false, class TWP = const cf*,
+          bool SKIP1 = false>
 __device__ __forceinline__ void pass_regs(cf* x, int k, TWP tw) {
   int S = 1;
-  if constexpr (R2) {
+  if constexpr (SKIP1) {
+    S = R2 ? 2 : 4;
+  } else if constexpr (R2) {
     constexpr int fs = N / (2 * MA);
 #pragma unroll
     for (int b = 0; b < R; b += 2) {
@@ -533,16 +538,30 @@ __device__ __forceinline__ void spec_factors(float rate, int l, v2f* F) {
 }
 // the window's samples times the factors (and the Hann window, LoRaDemod.cpp:158-160), in
 // pass-1 leaf order
-template <int SF, bool HANN>
+// FOLD: only the leading input of each of pass 1's first-stage butterflies (position p with
+// p % 4 == 0, or p % 2 == 0 for the odd-SF radix-2 stage) is multiplied here; the others keep
+// their samples (times the window) and hand their factor to fft_key<..., FOLD> as the
+// butterfly's twiddle (wz[p]).  The same rounding terms as the separate product (the bound's
+// rotation product and butterfly levels), in a different order.
+template <int SF, bool HANN, bool FOLD = false>
 __device__ __forceinline__ void spec_rotate_place(const cf* in, cf* z, const v2f* F, const float* __restrict__ win,
-                                                  int l) {
+                                                  int l, cf* wz = nullptr) {
   using G = Geo<SF>;
   constexpr int T = G::T, P = G::P, R1 = G::R1;
+  constexpr int LEAD = G::R2FIRST ? 2 : 4;  // first-stage butterfly span
 #pragma unroll
   for (int q = 0; q < P; ++q) {
-    cf v = unpk(pk_cmul(pk(in[q]), F[q]));
-    if constexpr (HANN) v = cscale(v, win[l + T * q]);
-    z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = v;
+    const int p = (q % G::G1) * R1 + leaf_pos(R1, q / G::G1);
+    if (FOLD && (p % LEAD) != 0) {
+      cf v = in[q];
+      if constexpr (HANN) v = cscale(v, win[l + T * q]);
+      z[p] = v;
+      wz[p] = unpk(F[q]);
+    } else {
+      cf v = unpk(pk_cmul(pk(in[q]), F[q]));
+      if constexpr (HANN) v = cscale(v, win[l + T * q]);
+      z[p] = v;
+    }
   }
 }
 
@@ -576,20 +595,38 @@ struct ConstTw1 {
 // CPRE: the pass-1 write-back positions c[h] (rev[l + T h] >> LOGR1) come from the caller
 // instead of vector loads.  FMA (the certified transforms): pass 1's twiddles are constants
 // (ConstTw1).
+// FOLD (certified symbol pass, spec_rotate_place<..., true>): pass 1's first stage takes the
+// rotation factors of its non-leading inputs as twiddles (wfold[p], position p in z) - their
+// inputs arrive unrotated - instead of the unit butterflies after a separate product: a
+// radix-4 stage 14 packed instructions per four points instead of 16, a radix-2 one 5 per
+// two instead of 6.
 template <int SF, bool KEEP, bool FMA = false, bool TWL = false, bool PACK = false, bool CPRE = false,
-          class HOOK = NoHook>
+          class HOOK = NoHook, bool FOLD = false>
 __device__ __forceinline__ uint64_t fft_key(cf* z, cf* row, int l, const KArgs& a, float* second = nullptr,
                                             const cf* twl = nullptr, const int* cpre = nullptr, HOOK hook = HOOK{},
-                                            const cf* wbpre = nullptr) {
+                                            const cf* wbpre = nullptr, const cf* wfold = nullptr) {
   using G = Geo<SF>;
   constexpr int N = G::N, T = G::T, P = G::P, R1 = G::R1;
   constexpr bool WL = G::WAVE_LOCAL;
+  static_assert(!FOLD || FMA, "the folded rotation is the certified path's");
 #pragma unroll
   for (int h = 0; h < G::G1; ++h) {
-    if constexpr (FMA)
+    if constexpr (FOLD) {
+      cf* x = z + h * R1;
+      const cf* w = wfold + h * R1;
+      if constexpr (G::R2FIRST) {
+#pragma unroll
+        for (int b = 0; b < R1; b += 2) bfly2<true>(x[b], x[b + 1], w[b + 1]);
+      } else {
+#pragma unroll
+        for (int b = 0; b < R1; b += 4) bfly4<true>(x[b], x[b + 1], x[b + 2], x[b + 3], w[b + 1], w[b + 2], w[b + 3]);
+      }
+      pass_regs<R1, G::R2FIRST, N, 1, !KEEP, FMA, ConstTw1<N>, true>(x, 0, ConstTw1<N>{});
+    } else if constexpr (FMA) {
       pass_regs<R1, G::R2FIRST, N, 1, !KEEP, FMA, ConstTw1<N>>(z + h * R1, 0, ConstTw1<N>{});
-    else
+    } else {
       pass_regs<R1, G::R2FIRST, N, 1, !KEEP, FMA>(z + h * R1, 0, a.tw);
+    }
   }
   uint64_t key = 0;
   if constexpr (G::NPASS == 1) {
@@ -987,6 +1024,9 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   constexpr int BPG = WL ? 4 : 1;         // blocks per workgroup round
   constexpr int NTW = demod_twl_entries<SF, true>();
   constexpr bool OSRN = OSRV != 1;
+  // the rotation folded into pass 1's first stage (fft_key FOLD): where the registers allow it
+  // (SF 9-12 and the windowed SF 6-8 kernels spill with the factors held until the stage)
+  constexpr bool FOLD = SF <= 8 && !HANN;
   static_assert(P == 16 && (MODE == 0 || MODE == 1), "SF >= 6, LEGACY (osr 1, or OSRN)");
   static_assert(OSRV == 0 || OSRV == 1 || OSRV == 2 || OSRV == 4, "osr 1, 2, 4 or run time");
   static_assert(NTW <= 256, "one staged twiddle per thread");
@@ -1163,14 +1203,15 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
     }
     }  // osr 1
-    cf z[P];
+    cf z[P], wz[P];
     {
       v2f F[P];
       spec_factors<SF>(rate, lr, F);
-      spec_rotate_place<SF, HANN>(in, z, F, a.win, lr);
+      spec_rotate_place<SF, HANN, FOLD>(in, z, F, a.win, lr, wz);
     }
     asm volatile("" : "+v"(pm));
-    const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true>(z, rows + (size_t)g * rowc, lr, a, nullptr, twl);
+    const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true, false, NoHook, FOLD>(
+        z, rows + (size_t)g * rowc, lr, a, nullptr, twl, nullptr, NoHook{}, nullptr, wz);
     // the symbol's best and runner-up keys over its lanes; the lane holding the best key
     // has the index (equal best keys in two lanes: a zero margin, so the symbol is
     // recomputed and overwritten)
@@ -1287,11 +1328,11 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
 #pragma unroll
       for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
       asm volatile("" : "+v"(pm));
-      cf z[P];
+      cf z[P], wz[P];
       {
         v2f F[P];
         spec_factors<SF>(B.rate, lr, F);
-        spec_rotate_place<SF, HANN>(in, z, F, a.win, lr);
+        spec_rotate_place<SF, HANN, FOLD>(in, z, F, a.win, lr, wz);
       }
       asm volatile("" : "+v"(pm));
       // the next block's samples, requested once this block's are consumed (their registers
@@ -1303,8 +1344,8 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       int cpre[G::G1];
 #pragma unroll
       for (int h = 0; h < G::G1; ++h) cpre[h] = __shfl(cown[h], lane0 + lr, 64);
-      const uint64_t lk =
-          fft_key<SF, false, true, (NTW > 0), true, true>(z, rows + (size_t)g * rowc, lr, a, nullptr, twl, cpre);
+      const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true, true, NoHook, FOLD>(
+          z, rows + (size_t)g * rowc, lr, a, nullptr, twl, cpre, NoHook{}, nullptr, wz);
       const uint32_t lbest = (uint32_t)lk;
       uint32_t best = lbest, sec = (uint32_t)(lk >> 32);
       spec_reduce<SF>(best, sec, pm, tid0, red3);
@@ -1409,11 +1450,11 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
 #pragma unroll
       for (int gg = 0; gg < P / G::RB; ++gg) load_tw2<G::RB, G::MA_B>(wb + gg * NTB, (lr + T * gg) % G::MA_B, a.twTB2);
       asm volatile("" : "+v"(pm));
-      cf z[P];
+      cf z[P], wz[P];
       {
         v2f F[P];
         spec_factors<SF>(B.rate, lr, F);
-        spec_rotate_place<SF, HANN>(in, z, F, a.win, lr);
+        spec_rotate_place<SF, HANN, FOLD>(in, z, F, a.win, lr, wz);
       }
       asm volatile("" : "+v"(pm));
       const int64_t bn = b + gstride * BPG;
@@ -1425,8 +1466,8 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       int cpre[G::G1];
 #pragma unroll
       for (int h = 0; h < G::G1; ++h) cpre[h] = d == 0 ? cown[h] : (int)(a.rev[lr + T * h] >> G::LOGR1);
-      const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true, true, decltype(hook)>(
-          z, rows + (size_t)g * rowc, lr, a, nullptr, twl, cpre, hook, wb);
+      const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true, true, decltype(hook), FOLD>(
+          z, rows + (size_t)g * rowc, lr, a, nullptr, twl, cpre, hook, wb, wz);
       const uint32_t lbest = (uint32_t)lk;
       uint32_t best = lbest, sec = (uint32_t)(lk >> 32);
       spec_reduce<SF>(best, sec, pm, tid0, red3);
