@@ -528,13 +528,21 @@ __device__ __forceinline__ void spec_factors(float rate, int l, v2f* F) {
   const float rev0 = __builtin_amdgcn_fractf((rate * (float)l) * INV_2PI);
   const float revd = __builtin_amdgcn_fractf((rate * (float)T) * INV_2PI);
   const float cd = __builtin_amdgcn_cosf(revd), sd = __builtin_amdgcn_sinf(revd);
-  // Written as plain vector arithmetic, not the v_pk_* asm helpers: the hazard recognizer
-  // does not see an asm instruction read a transcendental's result (gfx950 needs a wait
-  // state there), and the loop-invariant (-sd, sd) makes each step two packed operations.
+  // Plain vector arithmetic (scalar fp32 in this TU), at least for the first step: the
+  // hazard recognizer does not see an asm instruction read a transcendental's result (gfx950
+  // needs a wait state there), and that step's own operations put the distance between the
+  // sin/cos and any packed step after it.  SF 10-12 (16 factors per lane): the later steps
+  // two per asm statement (pk_cmul_chain2, the same operations bit for bit; SF12 symbol pass
+  // -0.3 %, SF7 +0.2 % - kept scalar there).
   const v2f wdr = {cd, cd}, wdi = {-sd, sd};
   F[0] = v2f{__builtin_amdgcn_cosf(rev0), __builtin_amdgcn_sinf(rev0)};
+  constexpr int QS = SF >= 10 ? 2 : P;  // first packed step
 #pragma unroll
-  for (int q = 1; q < P; ++q) F[q] = __builtin_elementwise_fma(F[q - 1].yx, wdi, F[q - 1] * wdr);
+  for (int q = 1; q < QS && q < P; ++q) F[q] = __builtin_elementwise_fma(F[q - 1].yx, wdi, F[q - 1] * wdr);
+  const v2f wd = {cd, sd};
+#pragma unroll
+  for (int q = QS; q + 1 < P; q += 2) pk_cmul_chain2(F[q - 1], wd, F[q], F[q + 1]);
+  if constexpr (QS < P && ((P - QS) % 2) == 1) F[P - 1] = pk_cmul(F[P - 2], wd);
 }
 // the window's samples times the factors (and the Hann window, LoRaDemod.cpp:158-160), in
 // pass-1 leaf order
@@ -549,6 +557,16 @@ __device__ __forceinline__ void spec_rotate_place(const cf* in, cf* z, const v2f
   using G = Geo<SF>;
   constexpr int T = G::T, P = G::P, R1 = G::R1;
   constexpr int LEAD = G::R2FIRST ? 2 : 4;  // first-stage butterfly span
+  if constexpr (SF >= 10 && !FOLD && !HANN && P % 2 == 0) {  // products two per asm statement
+#pragma unroll
+    for (int q = 0; q < P; q += 2) {
+      v2f r0, r1;
+      pk_cmul2(pk(in[q]), F[q], pk(in[q + 1]), F[q + 1], r0, r1);
+      z[(q % G::G1) * R1 + leaf_pos(R1, q / G::G1)] = unpk(r0);
+      z[((q + 1) % G::G1) * R1 + leaf_pos(R1, (q + 1) / G::G1)] = unpk(r1);
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < P; ++q) {
     const int p = (q % G::G1) * R1 + leaf_pos(R1, q / G::G1);

@@ -92,6 +92,28 @@ __device__ __forceinline__ v2f pk_cmul(v2f a, v2f w) {
       : "v"(a), "v"(w));
   return r;
 }
+// two independent products a0 * w0, a1 * w1 (pk_cmul's operations) in one asm statement:
+// one hazard pad per pair instead of one per product, the halves interleaved
+__device__ __forceinline__ void pk_cmul2(v2f a0, v2f w0, v2f a1, v2f w1, v2f& r0, v2f& r1) {
+  v2f t0, t1;
+  asm("v_pk_mul_f32 %2, %4, %5 op_sel_hi:[1,0]\n\t"
+      "v_pk_mul_f32 %3, %6, %7 op_sel_hi:[1,0]\n\t"
+      "v_pk_fma_f32 %0, %4, %5, %2 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\t"
+      "v_pk_fma_f32 %1, %6, %7, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+      : "=&v"(r0), "=v"(r1), "=&v"(t0), "=&v"(t1)
+      : "v"(a0), "v"(w0), "v"(a1), "v"(w1));
+}
+// two steps of a product recurrence, r0 = a * w, r1 = r0 * w (pk_cmul's operations), in one
+// asm statement
+__device__ __forceinline__ void pk_cmul_chain2(v2f a, v2f w, v2f& r0, v2f& r1) {
+  v2f t0, t1;
+  asm("v_pk_mul_f32 %2, %4, %5 op_sel_hi:[1,0]\n\t"
+      "v_pk_fma_f32 %0, %4, %5, %2 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\t"
+      "v_pk_mul_f32 %3, %0, %5 op_sel_hi:[1,0]\n\t"
+      "v_pk_fma_f32 %1, %0, %5, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+      : "=&v"(r0), "=v"(r1), "=&v"(t0), "=&v"(t1)
+      : "v"(a), "v"(w));
+}
 // c + a * w: (fma(-ai, wi, fma(ar, wr, cr)), fma(ar, wi, fma(ai, wr, ci)))
 __device__ __forceinline__ v2f pk_cfma(v2f a, v2f w, v2f c) {
   v2f t, r;
