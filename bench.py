@@ -211,13 +211,10 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     N = 1 << sf
     syms, iq = inputs if inputs is not None else make_input(sf, frames, data_syms, seed_base + rank, device,
                                                             snr_db, sync, osr)
-    if not spec:  # the three-launch path (frame max, estimate, demod), for comparison lines
-        os.environ["LORA_MI355X_SPEC"] = "0"
-    try:
+    # spec=False: the three-launch path (frame max, estimate, demod), for comparison lines
+    with amd.spec_pipeline(spec):
         plan = amd.DemodPlan(sf, osr, 125000, window, dechirp=True, mode="legacy", device=device,
                              precision=precision)
-    finally:
-        os.environ.pop("LORA_MI355X_SPEC", None)
     out = None
     for _ in range(warmup):
         out = plan.run(iq, out)

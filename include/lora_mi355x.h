@@ -190,6 +190,14 @@ int lora_demod_last_kernels(const lora_demod_plan* plan);
  * pipeline (three launches: frame max, estimate, demod). */
 int64_t lora_demod_spec_recomputed(lora_demod_plan* plan);
 
+/* Diagnostics of the C++ drop-in's private AQL queue (liblora_phy.so): with
+ * LORA_MI355X_AQL_PROFILE=1 set before the queue is created, every dispatch is timestamped
+ * and this returns the last call's timeline in microseconds relative to its doorbell:
+ * out[0] = packets n, out[1 + 2i], out[2 + 2i] = packet i's start and end on the GPU,
+ * out[1 + 2n] = when the host saw the completion.  Returns the doubles written (0 when
+ * nothing was profiled or cap < 2n + 2). */
+int lora_aql_last_profile(double* out, int cap);
+
 /* Thread-local text of the last error ("" if none). */
 const char* lora_last_error(void);
 

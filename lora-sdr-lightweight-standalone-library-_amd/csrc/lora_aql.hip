@@ -28,8 +28,10 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <mutex>
 #include <vector>
 
 #include "lora_internal.h"
@@ -61,6 +63,10 @@ struct AqlQueue {
   int nk = 0;
   bool hsa_up = false;
   bool broken = false;  // a call timed out with work in flight (aql_run refuses, -63)
+  // LORA_MI355X_AQL_PROFILE=1 at aql_create: one completion signal per packet and the
+  // queue's dispatch timestamps, read back after every call (lora_aql_last_profile)
+  bool prof = false;
+  hsa_signal_t psig[LaunchRecord::kMax]{};
 };
 
 namespace {
@@ -216,6 +222,26 @@ double now_s() {
   return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
 }
 
+// The last profiled aql_run (any queue, any thread; diagnostics only): packets, the
+// system-domain timestamps of the doorbell, each packet's start/end and the host's
+// observation of the completion.
+struct LastProfile {
+  std::mutex mu;
+  AqlQueue* q = nullptr;
+  int n = 0;
+  uint64_t bell = 0, seen = 0;
+};
+LastProfile& last_profile() {
+  static LastProfile p;
+  return p;
+}
+
+uint64_t sys_ts() {
+  uint64_t t = 0;
+  hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t);
+  return t;
+}
+
 }  // namespace
 
 int aql_create(int device, AqlQueue** out) {
@@ -272,6 +298,15 @@ int aql_create(int device, AqlQueue** out) {
       rc = -110;
       break;
     }
+    const char* pe = std::getenv("LORA_MI355X_AQL_PROFILE");
+    if (pe && pe[0] == '1' && hsa_amd_profiling_set_profiler_enabled(Q->q, 1) == HSA_STATUS_SUCCESS) {
+      Q->prof = true;
+      for (hsa_signal_t& sg : Q->psig)
+        if (hsa_signal_create(0, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) {
+          sg.handle = 0;
+          Q->prof = false;
+        }
+    }
     // this library's gfx950 code objects, loaded for the agent
     std::vector<unsigned char> file;
     std::vector<std::pair<size_t, size_t>> objs;
@@ -317,7 +352,14 @@ void aql_destroy(AqlQueue* Q) {
   // a queue whose kernels may still be running is left as it is (leaked): destroying it would
   // free the kernarg slots and the signal under them
   if (Q->broken) return;
+  {
+    LastProfile& P = last_profile();
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (P.q == Q) P.q = nullptr;
+  }
   if (Q->done.handle) hsa_signal_destroy(Q->done);
+  for (hsa_signal_t& sg : Q->psig)
+    if (sg.handle) hsa_signal_destroy(sg);
   if (Q->q) hsa_queue_destroy(Q->q);
   if (Q->kernarg) hsa_amd_memory_pool_free(Q->kernarg);
   for (int e = 0; e < Q->nexec; ++e) hsa_executable_destroy(Q->exec[e]);
@@ -352,6 +394,8 @@ int aql_run(AqlQueue* Q, const LaunchRecord& r) {
   while (base + n - hsa_queue_load_read_index_scacquire(q) > q->size) {
   }
   hsa_signal_store_relaxed(Q->done, 1);
+  if (Q->prof)
+    for (int i = 0; i + 1 < r.n; ++i) hsa_signal_store_relaxed(Q->psig[i], 1);
   hsa_kernel_dispatch_packet_t* ring = static_cast<hsa_kernel_dispatch_packet_t*>(q->base_address);
   for (int i = 0; i < r.n; ++i) {
     const RecordedLaunch& L = r.l[i];
@@ -381,7 +425,7 @@ int aql_run(AqlQueue* Q, const LaunchRecord& r) {
     p->kernel_object = ks[i]->object;
     p->kernarg_address = ka;
     p->reserved2 = 0;
-    p->completion_signal = i + 1 == r.n ? Q->done : hsa_signal_t{0};
+    p->completion_signal = i + 1 == r.n ? Q->done : (Q->prof ? Q->psig[i] : hsa_signal_t{0});
     // in order (barrier bit); system-scope acquire on the first packet (the host wrote the
     // samples) and release on the last (the host reads the outputs), agent scope between
     const uint16_t header =
@@ -392,6 +436,7 @@ int aql_run(AqlQueue* Q, const LaunchRecord& r) {
     const uint16_t setup = 1 << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
     __atomic_store_n(reinterpret_cast<uint32_t*>(p), (uint32_t)header | ((uint32_t)setup << 16), __ATOMIC_RELEASE);
   }
+  const uint64_t bell = Q->prof ? sys_ts() : 0;
   hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)(base + n - 1));
   // spin on the completion signal (the call is synchronous, like the reference's); give up
   // after 60 s rather than hang the caller
@@ -402,7 +447,42 @@ int aql_run(AqlQueue* Q, const LaunchRecord& r) {
       return -62;
     }
   }
+  if (Q->prof) {
+    // the packets' timestamps are read by lora_aql_last_profile, outside the caller's call
+    const uint64_t seen = sys_ts();
+    LastProfile& P = last_profile();
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.q = Q;
+    P.n = r.n;
+    P.bell = bell;
+    P.seen = seen;
+  }
   return 0;
 }
 
 }  // namespace lora
+
+// Diagnostics (include/lora_mi355x.h): the last profiled aql_run as microseconds relative
+// to its doorbell - out[0] = packets n, then per packet (start, end), then the host's
+// observation of the last completion.  Returns the doubles written (0: nothing profiled).
+extern "C" int lora_aql_last_profile(double* out, int cap) {
+  lora::LastProfile& P = lora::last_profile();
+  std::lock_guard<std::mutex> lk(P.mu);
+  if (!out || !P.q || P.n <= 0 || cap < 2 * P.n + 2) return 0;
+  uint64_t freq = 0;
+  if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq) != HSA_STATUS_SUCCESS || freq == 0) return 0;
+  const double us = 1e6 / (double)freq;
+  auto rel = [&](uint64_t t) { return ((double)t - (double)P.bell) * us; };
+  for (int i = 0; i < P.n; ++i) {
+    hsa_amd_profiling_dispatch_time_t t{};  // system-domain ticks
+    if (hsa_amd_profiling_get_dispatch_time(P.q->agent, i + 1 == P.n ? P.q->done : P.q->psig[i], &t) !=
+        HSA_STATUS_SUCCESS)
+      return 0;
+    out[1 + 2 * i] = rel(t.start);
+    out[2 + 2 * i] = rel(t.end);
+  }
+  out[0] = P.n;
+  out[1 + 2 * P.n] = rel(P.seen);
+  P.q = nullptr;  // read once: the next call reuses the signals
+  return 2 * P.n + 2;
+}

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "../../include/lora_mi355x.h"
+#include "lora_chirp.h"
 #include "lora_device.h"
 #include "lora_internal.h"
 
@@ -670,6 +671,180 @@ __global__ void __launch_bounds__(kModLanes * kModWaves) k_mod_samples(ModArgs a
   }
 }
 
+
+// ---- few frames: one workgroup per frame (k_mod_frame) ------------------------------
+// With few frames the bulk kernels above leave the chip idle while one lane per frame
+// walks the whole frame's recurrence at five dependent operations per sample (SF7, one
+// frame: ~180 us).  Here a frame's samples go through windows of <= 4096 samples in a
+// three-stage pipeline over one workgroup:
+//   * waves 1-3 fill window t+1 with its frequencies - short chirps (< kMfTabMin samples)
+//     by one lane per chirp running the frequency recurrence, long ones from the runs of
+//     lora_chirp.h (built one window ahead by a few lanes, then evaluated in parallel);
+//   * lane 0 of wave 0 turns window t's frequencies into phases in place - the one truly
+//     sequential part, a single dependent fp32 add per sample (ChirpGenerator.hpp:121)
+//     plus the per-chirp wrap (:130);
+//   * waves 1-3 evaluate window t-1's samples (glibc-exact sincosf, :122) and store them.
+// Results are the recurrence's own, bit for bit (the runs are exact, chirp_seg_check).
+constexpr int kMfWin = 4096;     // samples per window (whole chirps, or an exact fraction of one)
+constexpr int kMfTabMin = 1024;  // chirps of at least this many samples take runs
+constexpr int kMfTabChirps = kMfWin / kMfTabMin;  // long chirps per window
+constexpr int kMfSegMax = 92;    // runs per chirp: lora::chirp_seg_cap(12)
+static_assert(kMfSegMax >= lora::chirp_seg_cap(12), "run table per chirp");
+constexpr int kMfThreads = 256;
+constexpr int kMfWorkers = kMfThreads - 64;
+constexpr int64_t kMfMaxFrames = 512;  // at most this many frames take k_mod_frame
+
+// window t's table group: a window of whole chirps is its own group, the windows of one
+// long chirp share the chirp's
+__device__ __forceinline__ int mf_group(int t, int W, int step) { return step <= W ? t : (int)((int64_t)t * W / step); }
+
+__global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int nwin) {
+  __shared__ __attribute__((aligned(16))) float buf[3][kMfWin];
+  __shared__ lora::ChirpSeg tab[2][kMfTabChirps][kMfSegMax];
+  __shared__ int tcnt[2][kMfTabChirps];
+  const int64_t fr = blockIdx.x;
+  cf* out = a.iq + fr * (int64_t)a.nchirp * a.step;
+  const int tid = threadIdx.x;
+  const int wk = tid - 64;  // worker index (waves 1-3), < 0 in wave 0
+  const lora::ChirpConst cc{a.fMin, a.fMax, a.fStep, a.fMax - a.fMin};
+  const int64_t total = (int64_t)a.nchirp * a.step;
+  const bool runs = a.step >= kMfTabMin;
+  const int cap = lora::chirp_seg_cap(31 - __builtin_clz((unsigned)a.N));
+  // runs of the long chirps starting in window t, into slot group(t) % 2, by the last
+  // workers (the others fill and evaluate meanwhile)
+  const int nbuild = runs ? (a.step <= W ? W / a.step : 1) : 0;
+  const int nwk = kMfWorkers - nbuild;  // workers that fill and evaluate
+  auto build = [&](int t) {
+    const int j = wk - nwk;
+    if (!runs || j < 0 || t >= nwin) return;
+    if (t > 0 && mf_group(t, W, a.step) == mf_group(t - 1, W, a.step)) return;  // same chirp
+    const int64_t s0 = (int64_t)t * W;
+    const int c = (int)(s0 / a.step) + j;
+    if (c >= a.nchirp || (int64_t)c * a.step >= s0 + W) return;
+    const int slot = mf_group(t, W, a.step) & 1;
+    tcnt[slot][j] = lora::chirp_segments(a.fMin + chirp_f0(a, fr, c), a.step, cc, tab[slot][j], cap);
+  };
+  // window t's frequencies into buf[t % 3]
+  auto fill = [&](int t) {
+    if (wk < 0 || wk >= nwk || t >= nwin) return;
+    const int64_t s0 = (int64_t)t * W;
+    const int n = (int)min((int64_t)W, total - s0);
+    float* b = buf[t % 3];
+    if (!runs) {
+      // whole short chirps, one lane each: the recurrence itself
+      for (int c = wk; c < n / a.step; c += nwk) {
+        float f = a.fMin + chirp_f0(a, fr, (int)(s0 / a.step) + c);
+        float* bc = b + c * a.step;
+        for (int k = 0; k < a.step; ++k) {
+          f = lora::chirp_fstep(f, cc);
+          bc[k] = f;
+        }
+      }
+      return;
+    }
+    const int slot = mf_group(t, W, a.step) & 1;
+    const int per = (n + nwk - 1) / nwk;
+    int i = wk * per;
+    const int i1 = min(n, i + per);
+    while (i < i1) {
+      const int64_t g = s0 + i;
+      const int c = (int)(g / a.step);
+      const int j = c - (int)(s0 / a.step);  // the chirp's table in the slot
+      int k = (int)(g - (int64_t)c * a.step) + 1;
+      const int iend = min(i1, i + (a.step - k + 1));
+      const int ns = tcnt[slot][j];
+      if (ns < 0) {
+        // (runs overflowed their cap - a start frequency far outside [fMin, fMax], a
+        // symbol >= N: the recurrence from the chirp's start)
+        float f = a.fMin + chirp_f0(a, fr, c);
+        for (int q = 0; q < k - 1; ++q) f = lora::chirp_fstep(f, cc);
+        for (; i < iend; ++i) {
+          f = lora::chirp_fstep(f, cc);
+          b[i] = f;
+        }
+        continue;
+      }
+      const lora::ChirpSeg* S = tab[slot][j];
+      int lo = 0, hi = ns - 1;  // the last run with k0 <= k
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (S[mid].k0 <= k) lo = mid;
+        else hi = mid - 1;
+      }
+      for (; i < iend; ++i, ++k) {
+        while (k >= S[lo].k0 + S[lo].len) ++lo;
+        b[i] = lora::chirp_seg_f(S[lo], k);
+      }
+    }
+  };
+  // window t's phases in place (lane 0 only)
+  auto chain = [&](int t, float& phase) {
+    const int64_t s0 = (int64_t)t * W;
+    const int n = (int)min((int64_t)W, total - s0);
+    float* b = buf[t % 3];
+    const int len = a.step <= W ? a.step : n;  // samples until the next chirp boundary
+    for (int c0 = 0; c0 < n; c0 += len) {
+      float* bc = b + c0;
+      if ((len & 15) == 0) {
+        float4 x[4], y[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = reinterpret_cast<const float4*>(bc)[q];
+        for (int i = 0; i < len; i += 16) {
+          if (i + 16 < len) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) y[q] = reinterpret_cast<const float4*>(bc + i + 16)[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            phase += x[q].x;
+            x[q].x = phase;
+            phase += x[q].y;
+            x[q].y = phase;
+            phase += x[q].z;
+            x[q].z = phase;
+            phase += x[q].w;
+            x[q].w = phase;
+            reinterpret_cast<float4*>(bc + i)[q] = x[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[q] = y[q];
+        }
+      } else {
+        for (int i = 0; i < len; ++i) {
+          phase += bc[i];
+          bc[i] = phase;
+        }
+      }
+      // ChirpGenerator.hpp:130 at each chirp's end
+      if ((s0 + c0 + len) % a.step == 0) phase = (float)((double)phase - floor((double)phase / (2 * M_PI)) * 2 * M_PI);
+    }
+  };
+  // window t's samples (ChirpGenerator.hpp:122: polar(ampl, phase))
+  auto emit = [&](int t) {
+    if (wk < 0 || wk >= nwk) return;
+    const int64_t s0 = (int64_t)t * W;
+    const int n = (int)min((int64_t)W, total - s0);
+    const float* b = buf[t % 3];
+    for (int i = wk; i < n; i += nwk) {
+      float sn, cs;
+      lm_sincosf_bf(b[i], &sn, &cs);
+      out[s0 + i] = cf{a.ampl * cs, a.ampl * sn};
+    }
+  };
+  float phase = 0.0f;
+  build(0);
+  __syncthreads();
+  for (int t = 0; t < nwin + 2; ++t) {
+    if (wk < 0) {
+      if (tid == 0 && t >= 1 && t - 1 < nwin) chain(t - 1, phase);
+    } else {
+      fill(t);
+      build(t + 1);
+      if (t >= 2) emit(t - 2);
+    }
+    __syncthreads();
+  }
+}
 }  // namespace
 
 // ===================================================================================
@@ -1184,10 +1359,17 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
   // short ones 64 frames per wave (their chains are short: the lanes' issue count matters)
   a.fpw = step >= 1024 ? 1 : 64;
   while (a.fpw < 64 && (int64_t)a.fpw * 1024 < frames) a.fpw *= 2;
-  lora::launch(k_mod_phase, dim3((unsigned)((frames + a.fpw - 1) / a.fpw)), dim3(64), 0, st, a);
-  const int64_t chirps = frames * a.nchirp;
-  const int64_t per_block = (int64_t)kModLanes * kModWaves;
-  lora::launch(k_mod_samples, dim3((unsigned)((chirps + per_block - 1) / per_block)), dim3(per_block), 0, st, a);
+  if (frames <= kMfMaxFrames) {
+    // few frames: a workgroup per frame, windows of whole chirps or exact chirp fractions
+    const int W = step <= kMfWin ? step * (kMfWin / step) : step / ((step + kMfWin - 1) / kMfWin);
+    const int64_t nwin = (per_frame + W - 1) / W;
+    lora::launch(k_mod_frame, dim3((unsigned)frames), dim3(kMfThreads), 0, st, a, W, (int)nwin);
+  } else {
+    lora::launch(k_mod_phase, dim3((unsigned)((frames + a.fpw - 1) / a.fpw)), dim3(64), 0, st, a);
+    const int64_t chirps = frames * a.nchirp;
+    const int64_t per_block = (int64_t)kModLanes * kModWaves;
+    lora::launch(k_mod_samples, dim3((unsigned)((chirps + per_block - 1) / per_block)), dim3(per_block), 0, st, a);
+  }
   hipError_t e = hipGetLastError();
   if (prev != device) hipSetDevice(prev);
   if (e != hipSuccess) return set_error(LORA_EIO, std::string("mod launch: ") + hipGetErrorString(e));

@@ -12,6 +12,12 @@
 #include "../../include/lora_mi355x_phy.hpp"
 #include "lora_internal.h"
 
+namespace lora_phy {
+namespace detail {
+void ensure_runtime();  // the drop-in runtime's set-up, once (below)
+}
+}  // namespace lora_phy
+
 namespace {
 
 // Hamming 8/4 of LoRaCodes.hpp:229-281 (encodeHamming84sx / decodeHamming84sx): data bits
@@ -239,6 +245,11 @@ int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* 
   o.cfo = reinterpret_cast<float*>(host + d.cfo);
   o.time_offset = reinterpret_cast<float*>(host + d.toff);
   o.max_amp = reinterpret_cast<float*>(host + d.maxa);
+  // The runtime's queue and plans are shared by every borrowing workspace: one frame at a
+  // time through them (lora_demod_batch writes the plan's bookkeeping - last_kernels, the
+  // recompute counter's reads - and the queue takes one dispatch at a time).
+  std::unique_lock<std::mutex> lk(rt().mu, std::defer_lock);
+  if (g.shared_aql || g.shared_plan) lk.lock();
   lora::LaunchRecord rec;
   lora::t_launch_record = &rec;
   const int64_t rc = lora_demod_batch(g.plan, reinterpret_cast<const float*>(host + d.iq), 1, (int64_t)count,
@@ -247,12 +258,10 @@ int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* 
   if (rc < 0) return 0;
   if (rec.bad) return -1;
   if (rec.n > 0) {
-    // the runtime's queue is shared by every borrowing workspace: one dispatch at a time
-    std::unique_lock<std::mutex> lk(rt().mu, std::defer_lock);
-    if (g.shared_aql) lk.lock();
     const int e = lora::aql_run(static_cast<lora::AqlQueue*>(g.aql), rec);
     if (e != 0) return e;
   }
+  lk.unlock();
   out.nsym = nsym;
   out.sync = host[d.sync];
   std::memcpy(&out.cfo, host + d.cfo, 4);
@@ -279,13 +288,15 @@ bool run_frame(lora_phy::detail::device_state& g, const std::complex<float>* sam
       // and write the outputs there, so the queue and both buffers are abandoned (leaked;
       // a borrowed slot stays busy) and this and later frames take the HIP path on fresh
       // buffers
+      // (the slot's stream stays with the abandoned slot too: this workspace gets its own)
+      if (g.slot >= 0 && g.stream == rt().slots[g.slot].stream) g.stream = nullptr;
       g.aql = nullptr;
       g.shared_aql = false;
       g.aql_status = -62;
       g.slot = -1;
       g.dev = g.host = nullptr;
       g.bytes = g.samples = 0;
-      if (!ensure_buffers(g, std::max<size_t>(count, 1))) return false;
+      if (!ensure_stream(g) || !ensure_buffers(g, std::max<size_t>(count, 1))) return false;
       return run_frame(g, samples, count, out, false);
     }
     // -1 (a launch the queue does not take) and every error raised before a packet is
@@ -403,6 +414,7 @@ bool borrow(detail::device_state& g, unsigned sf, int window, size_t max_samples
 void lora_demod_init(lora_demod_workspace* ws, unsigned sf, window_type win, std::complex<float>* scratch,
                      size_t max_samples) {
   if (!ws) return;
+  detail::ensure_runtime();
   // the reference's init overwrites every field: a workspace initialised before (for any
   // sf / window) gives up its device resources first
   detail::release(ws->gpu);
@@ -458,6 +470,7 @@ void lora_demod_free(lora_demod_workspace* ws) {
 size_t lora_demodulate(lora_demod_workspace* ws, const std::complex<float>* samples, size_t sample_count,
                        uint16_t* out_symbols, unsigned osr, uint8_t* out_sync) {
   if (!ws || ws->N == 0 || !samples) return 0;
+  detail::ensure_runtime();
   if (osr == 0) osr = 1;
   unsigned sf = 0;
   while ((size_t(1) << sf) < ws->N) ++sf;
@@ -483,6 +496,7 @@ size_t lora_modulate(const uint16_t* symbols, size_t symbol_count, std::complex<
   if (sf < 2 || sf > 12) return 0;
   const size_t per = (symbol_count + 2) * (size_t(1) << sf) * osr;
   if (!out_samples || (symbol_count > 0 && !symbols)) return 0;
+  detail::ensure_runtime();
   Runtime& R = rt();
   if (R.up && R.aql && per <= kModSamples && symbol_count <= kModSyms) {
     // the runtime's pinned staging (symbols | IQ), which the kernels read and write in place,
@@ -555,6 +569,7 @@ size_t lora_decode(const uint16_t* symbols, size_t symbol_count, uint8_t* out_by
 
 int init(lora_workspace* ws, const lora_params* cfg) {
   if (!ws || !cfg) return -1;                  // phy.cpp:27
+  detail::ensure_runtime();
   if (cfg->sf < 2 || cfg->sf > 12) return -1;  // kissfft's static plans hold N <= 4096 (kissfft.hh:34)
   const unsigned bw_hz = static_cast<unsigned>(cfg->bw);
   if (bw_hz != 125000 && bw_hz != 250000 && bw_hz != 500000) return -1;
@@ -711,13 +726,13 @@ int genChirp(std::complex<float>* samps, int N, int osr, int NN, float f0, bool 
 // every call on its own allocating path.
 // ---------------------------------------------------------------------------------------
 namespace {
+thread_local bool t_in_setup = false;  // runtime_setup's own warm-up calls (no re-entry)
 void runtime_setup() {
+  t_in_setup = true;
+  struct Done {
+    ~Done() { t_in_setup = false; }
+  } done;
   Runtime& R = rt();
-  const char* lazy = std::getenv("LORA_MI355X_DROPIN_LAZY");
-  if (lazy && lazy[0] == '1') {
-    R.status = 1;
-    return;
-  }
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
     R.status = 2;
@@ -805,10 +820,35 @@ void runtime_setup() {
     }
   }
 }
-__attribute__((constructor)) void lora_phy_dropin_load() { runtime_setup(); }
+// LORA_MI355X_DROPIN_LAZY=1 defers the set-up from load time to the first drop-in call that
+// needs the GPU (ensure_runtime): a process that loads liblora_phy.so then has no GPU state
+// before that call, so it may still fork and exec before it (performance_test.cpp:71 runs
+// std::system("mkdir -p logs") first) - at the price of that first call allocating.
+bool lazy_setup() {
+  const char* lazy = std::getenv("LORA_MI355X_DROPIN_LAZY");
+  return lazy && lazy[0] == '1';
+}
+std::once_flag g_setup_once;
+__attribute__((constructor)) void lora_phy_dropin_load() {
+  if (lazy_setup()) {
+    rt().status = 1;
+    return;
+  }
+  std::call_once(g_setup_once, runtime_setup);
+}
 }  // namespace
 
-// 0 when the load-time runtime is up, else the step that failed (1: disabled by
-// LORA_MI355X_DROPIN_LAZY, 2: no HIP device, 3-6: plans / buffers, a negative aql_create
+namespace lora_phy {
+namespace detail {
+// Every drop-in entry point that touches the GPU calls this first: a no-op once the
+// load-time set-up ran; under LORA_MI355X_DROPIN_LAZY=1 the first call runs it here.
+void ensure_runtime() {
+  if (!t_in_setup) std::call_once(g_setup_once, runtime_setup);
+}
+}  // namespace detail
+}  // namespace lora_phy
+
+// 0 when the load-time runtime is up, else the step that failed (1: deferred by
+// LORA_MI355X_DROPIN_LAZY and no drop-in call made yet, 2: no HIP device, 3-6: plans / buffers, a negative aql_create
 // code, 7-8 / -13x: the warm-up)
 extern "C" int lora_phy_dropin_status(void) { return rt().status; }

@@ -8,11 +8,11 @@ is in :mod:`lora_phy_amd.phy`.
 """
 from . import _capi, codes, iq_io, phy, shard  # noqa: F401
 from ._capi import LoraError
-from .demod import DemodPlan, DemodResult, LoRaDemod, compensate_offsets
+from .demod import DemodPlan, DemodResult, LoRaDemod, compensate_offsets, spec_pipeline
 from .mod import LoRaMod, modulate
 
 __all__ = ["DemodPlan", "DemodResult", "LoRaDemod", "LoRaMod", "LoraError", "modulate",
-           "compensate_offsets", "codes", "iq_io", "phy", "shard", "lib_path", "version", "source_hash",
+           "compensate_offsets", "spec_pipeline", "codes", "iq_io", "phy", "shard", "lib_path", "version", "source_hash",
            "check_build"]
 
 

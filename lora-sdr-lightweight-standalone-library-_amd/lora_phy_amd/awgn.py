@@ -151,13 +151,10 @@ def sweep_chain(sf: int, snr_dbs: Sequence[float], frames: int = 1000, payload_l
     plan = DemodPlan(sf, osr, 125000, "none", dechirp=True, mode="legacy", device=dev)
     xplan = None
     if exact_check:
-        import os
+        from .demod import spec_pipeline
 
-        os.environ["LORA_MI355X_SPEC"] = "0"
-        try:
+        with spec_pipeline(False):
             xplan = DemodPlan(sf, osr, 125000, "none", dechirp=True, mode="legacy", device=dev)
-        finally:
-            os.environ.pop("LORA_MI355X_SPEC", None)
     gen = torch.Generator(device=dev).manual_seed(seed + 1)
     out = []
     for snr in snr_dbs:

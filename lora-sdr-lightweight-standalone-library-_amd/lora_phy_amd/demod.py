@@ -7,7 +7,9 @@ caller; outputs are allocated with torch's caching allocator (no hipMalloc per c
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -250,3 +252,21 @@ class LoRaDemod:
         if self.last is None:
             raise RuntimeError("work() has not run")
         return self.last.sync == self.sync
+
+
+@contextlib.contextmanager
+def spec_pipeline(enabled: bool = True):
+    """Plans created inside this block use the speculative single-read pipeline (the
+    default) or, with ``enabled=False``, the three-launch exact path (frame max, estimate,
+    demod: ``LORA_MI355X_SPEC=0``, read by lora_demod_plan_create).  The caller's own value
+    of the variable is restored on exit, not removed."""
+    prev = os.environ.get("LORA_MI355X_SPEC")
+    if not enabled:
+        os.environ["LORA_MI355X_SPEC"] = "0"
+    try:
+        yield
+    finally:
+        if prev is None:
+            os.environ.pop("LORA_MI355X_SPEC", None)
+        else:
+            os.environ["LORA_MI355X_SPEC"] = prev

@@ -24,7 +24,6 @@ def test_configs4_shape_every_chunk_vs_oracle(path):
     (LORA_MI355X_SPEC=0) with the one-wave-per-frame max pass."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    import os
     import lora_phy_amd as amd
     from oracle.pyoracle import Oracle
 
@@ -46,12 +45,8 @@ def test_configs4_shape_every_chunk_vs_oracle(path):
         x += torch.view_as_complex(torch.randn((n, L, 2), generator=gn, device=dev)) * sig
         iq[r0:r0 + n] = x
         del x
-    if path == "split":
-        os.environ["LORA_MI355X_SPEC"] = "0"
-    try:
+    with amd.spec_pipeline(path != "split"):
         plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=dev)
-    finally:
-        os.environ.pop("LORA_MI355X_SPEC", None)
     want = {"spec", "estimate", "demod"} if path == "spec" else {"frame_max", "frame_max_wave", "estimate", "demod"}
     per_chunk = int(8e9 // (L * 8))
     chunks = [(c0, min(per_chunk, frames - c0)) for c0 in range(0, frames, per_chunk)]

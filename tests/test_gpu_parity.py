@@ -89,14 +89,8 @@ def make_plan(amd, path, *args, **kw):
     pipeline wherever it covers the configuration (LEGACY, osr 1, SF >= 6,
     >= 3 symbols, either window); "split": the same kernels as three launches (frame max, estimate,
     demod: LORA_MI355X_SPEC=0, the one diagnostic knob)."""
-    import os
-
-    if path == "split":
-        os.environ["LORA_MI355X_SPEC"] = "0"
-    try:
+    with amd.spec_pipeline(path != "split"):
         return amd.DemodPlan(*args, **kw)
-    finally:
-        os.environ.pop("LORA_MI355X_SPEC", None)
 
 
 @pytest.mark.parametrize("path", ["fast", "split"])
@@ -179,6 +173,27 @@ def test_modulator_many_frames_matches_oracle(O, amd, sf, frames):
     for f in (0, 1, 63, 64, frames // 2, frames - 2, frames - 1):
         ref = O.lora_modulate(syms[f], sf, 1, 125000, 1.0, 0x12)
         np.testing.assert_array_equal(iq[f].cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("sf,osr,S,frames,big", [(7, 1, 64, 1, False), (7, 1, 64, 1, True), (8, 3, 40, 3, True),
+                                                  (10, 1, 30, 2, True), (11, 3, 6, 2, False), (12, 1, 10, 1, True),
+                                                  (12, 4, 3, 2, False), (2, 1, 50, 4, True), (9, 2, 20, 512, False),
+                                                  (9, 2, 20, 513, False)])
+def test_modulator_frame_kernel_matches_oracle(O, amd, sf, osr, S, frames, big):
+    """Up to 512 frames take k_mod_frame (a workgroup per frame: frequencies from the runs of
+    csrc/lora_chirp.h or the per-chirp recurrence, one lane's phase chain, parallel sincosf)
+    - 513 the bulk kernels.  Windows of whole chirps and of chirp fractions (osr 3/4 at
+    SF 11/12), partial last windows, and symbols >= N (lora_encode's codewords reach 255;
+    `big`: uint16 values up to 65535, whose chirps may overflow the run table and fall back
+    to the recurrence) - every sample bit for bit against the oracle."""
+    rng = np.random.default_rng(sf * 131 + osr + frames)
+    hi = 65536 if big else (1 << sf)
+    syms = rng.integers(0, hi, (frames, S)).astype(np.uint16)
+    bw = 250000 if sf == 10 else 125000
+    iq = amd.modulate(torch.from_numpy(syms.astype(np.int32)).cuda(), sf, osr, bw, 1.0, 0x12).cpu().numpy()
+    for f in sorted({0, frames // 2, frames - 1}):
+        ref = O.lora_modulate(syms[f], sf, osr, bw, 1.0, 0x12)
+        np.testing.assert_array_equal(iq[f].view(np.uint32), ref.view(np.uint32))
 
 
 def test_modulator_into_a_preallocated_buffer(amd):

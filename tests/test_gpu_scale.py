@@ -16,7 +16,6 @@ frames.
 Reference: /root/reference/src/phy/LoRaDemod.cpp:137-175 (the per-symbol loop the
 certification must reproduce), tests/awgn_sweep.py:245-273 (the SNR model).
 """
-import os
 
 import numpy as np
 import pytest
@@ -76,12 +75,8 @@ def noisy_batch(amd, sf, F, S, snr_db, cfo_bins, seed, chunk=8192):
 
 
 def plan_for(amd, sf, spec):
-    if not spec:
-        os.environ["LORA_MI355X_SPEC"] = "0"
-    try:
+    with amd.spec_pipeline(spec):
         return amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy")
-    finally:
-        os.environ.pop("LORA_MI355X_SPEC", None)
 
 
 @pytest.mark.parametrize("sf,F", [(7, 100_000), (12, 2_000)])

@@ -47,14 +47,8 @@ def bits(x):
 def check(O, amd, iq, sf, spec=True):
     """Run `iq` ([F, L] dechirped frames) through a fresh plan and compare every output
     with the oracle; returns (plan, recomputed symbols).  spec=False: three-launch path."""
-    import os
-
-    if not spec:
-        os.environ["LORA_MI355X_SPEC"] = "0"
-    try:
+    with amd.spec_pipeline(spec):
         plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=False)
-    finally:
-        os.environ.pop("LORA_MI355X_SPEC", None)
     res = plan.run(torch.from_numpy(np.ascontiguousarray(iq)).cuda())
     torch.cuda.synchronize()
     syms = res.symbols.cpu().numpy()
@@ -259,8 +253,6 @@ def test_max_amp_is_the_reference_frame_maximum(O, amd, sf, dechirp, path):
     drives: the pipeline assembles it from window maxima of exactly-dechirped samples (the
     demod's fused multiply-adds must not reach them).  Frames of random symbols at random
     amplitude around 1, some with a ragged tail."""
-    import os
-
     N = 1 << sf
     S = 6 if sf < 12 else 4
     F = 48 if sf < 12 else 8
@@ -276,12 +268,8 @@ def test_max_amp_is_the_reference_frame_maximum(O, amd, sf, dechirp, path):
             x = O.dechirp(x.astype(np.complex64), sf, 1)
         iq[f, : S * N] = x.astype(np.complex64)
         iq[f, S * N:] = (0.3 * rng.standard_normal(L - S * N)).astype(np.complex64)
-    if path == "split":
-        os.environ["LORA_MI355X_SPEC"] = "0"
-    try:
+    with amd.spec_pipeline(path != "split"):
         plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=dechirp)
-    finally:
-        os.environ.pop("LORA_MI355X_SPEC", None)
     res = plan.run(torch.from_numpy(iq).cuda())
     torch.cuda.synchronize()
     assert ("spec" in plan.last_kernels()) == (path != "split")
