@@ -203,7 +203,12 @@ def stage_times(plan, iq, out, steps, device):
 
 
 def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, precision="exact",
-               inputs=None, sync=None, seed_base=20251015, rank=0, window="none", osr=1, spec=True):
+               inputs=None, sync=None, seed_base=20251015, rank=0, window="none", osr=1, spec=True,
+               mode="legacy"):
+    """mode "legacy": lora_demodulate with the fused caller dechirp (the headline); "api":
+    lora_phy::demodulate (phy.cpp:178-239: estimate on the raw samples, down-chirp fused per
+    symbol); "raw": the detector alone per symbol (dechirp -> FFT -> argmax, the AWGN
+    script's receiver, tests/awgn_sweep.py:262-273), every symbol of the frame an output."""
     import torch
 
     import lora_phy_amd as amd
@@ -213,7 +218,7 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
                                                             snr_db, sync, osr)
     # spec=False: the three-launch path (frame max, estimate, demod), for comparison lines
     with amd.spec_pipeline(spec):
-        plan = amd.DemodPlan(sf, osr, 125000, window, dechirp=True, mode="legacy", device=device,
+        plan = amd.DemodPlan(sf, osr, 125000, window, dechirp=True, mode=mode, device=device,
                              precision=precision)
     out = None
     for _ in range(warmup):
@@ -249,12 +254,20 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     fixed = (plan.spec_recomputed() - fixed0) / steps
     kernels = sorted(plan.last_kernels())
     stage_ms, out = stage_times(plan, iq, out, steps, device)
-    wall_max, units = all_max_sum(dist, wall, frames * data_syms * steps)
     total_syms = data_syms + 2
+    # RAW mode demodulates every symbol of the frame (the sync symbols too)
+    out_syms = total_syms if mode == "raw" else data_syms
+    wall_max, units = all_max_sum(dist, wall, frames * out_syms * steps)
     ms_step = wall * 1e3 / steps
     B_sym = 8 * N * osr + 2
     got = out.symbols.to(torch.int32).cpu()
-    ser = float((got != syms).float().mean())
+    if mode == "raw":
+        sw = SYNC if sync is None else sync
+        shift = sf - 4 if sf > 4 else 0
+        head = torch.tensor([(sw >> 4) << shift, (sw & 0xF) << shift], dtype=torch.int32)
+        ser = float((got != torch.cat([head.expand(frames, 2), syms], 1)).float().mean())
+    else:
+        ser = float((got != syms).float().mean())
     # the symbol pass in the speculative pipeline (ranks sharing a device in a rehearsal
     # can distort the stage times); otherwise the longest stage
     dom = 2 if "spec" in kernels else max(range(3), key=lambda k: stage_ms[k])
@@ -270,19 +283,21 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
                  1: frames * (2 * W + 9),                     # estimate: symbols 0/1 + outputs
                  2: (frames * (total_syms * W + 2 * data_syms) if spec
                      # three-launch demod: every osr-th sample of a window is read
-                     else frames * data_syms * (8 * N + 2))}[dom]
+                     else frames * out_syms * (8 * N + 2))}[dom]
     dom_gbs = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9
     return {
-        "sf": sf, "osr": osr, "frames": frames, "data_symbols": frames * data_syms, "iq_bytes": iq.numel() * 8,
+        "sf": sf, "osr": osr, "mode": mode, "window": window, "precision": precision,
+        "frames": frames, "data_symbols": frames * out_syms, "iq_bytes": iq.numel() * 8,
         "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ser == 0.0, "ser_vs_tx": ser,
         "kernels": kernels, "spec_recomputed_per_step": fixed,
-        "msym_s_data": frames * data_syms / (ms_step * 1e-3) / 1e6,
+        "msym_s_data": frames * out_syms / (ms_step * 1e-3) / 1e6,
         "msym_s_all_ranks": units / wall_max / 1e6, "ms_per_step_max_rank": wall_max * 1e3 / steps,
         "msym_s_all": frames * total_syms / (ms_step * 1e-3) / 1e6,
         # stage 2 is the symbol pass: k_spec_demod in the speculative pipeline (the default),
         # k_demod_fast in the three-launch one
         "dominant_kernel": ["k_frame_max", "k_est_fast",
                             "k_spec_demod" if "spec" in kernels else "k_demod_fast"][dom], "dominant_stage": dom,
+        "sync": SYNC if sync is None else sync,
         "dominant_gbs": dom_gbs, "dominant_bytes_per_launch": dom_bytes,
         "step_bytes": step_bytes, "pipeline_gbs": step_bytes / (ms_step * 1e-3) / 1e9,
         "plan": plan, "iq": iq, "syms": syms, "out": out,
@@ -291,6 +306,88 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
 
 def public(r):
     return {k: v for k, v in r.items() if k not in ("plan", "iq", "syms", "out")}
+
+
+def _bits(t):
+    import torch
+
+    return t.contiguous().view(torch.int32)
+
+
+def exact_parity(r, device, ref=None):
+    """Parity of a line measured in the run: every frame's outputs (symbols, sync word and
+    the fp32 bits of cfo / time_offset) against the three-launch exact path on the same
+    batch (frame max, estimate, demod with glibc-faithful sincosf: LORA_MI355X_SPEC=0, the
+    path the GPU test suite pins to the oracle and the reference bit for bit).  `ref`: an
+    already computed exact run of the same inputs (its DemodResult)."""
+    import torch
+
+    import lora_phy_amd as amd
+
+    if ref is None:
+        with amd.spec_pipeline(False):
+            plan = amd.DemodPlan(r["sf"], r["osr"], 125000, r["window"], dechirp=True, mode=r["mode"], device=device,
+                                 precision="exact")
+        ref = plan.run(r["iq"])
+        torch.cuda.synchronize(device)
+        del plan
+    o = r["out"]
+    bad = (o.symbols.to(torch.int32) != ref.symbols.to(torch.int32)).any(1) | (o.sync != ref.sync)
+    bad |= (_bits(o.cfo) != _bits(ref.cfo)) | (_bits(o.time_offset) != _bits(ref.time_offset))
+    nbad = int(bad.sum())
+    return {"parity_ok": nbad == 0, "frames_compared": int(o.symbols.shape[0]), "frames_mismatched": nbad,
+            "vs": "three-launch exact path on the same batch (LORA_MI355X_SPEC=0; oracle-pinned by the GPU tests)"}
+
+
+def reference_leg(r, nframes=32, budget_s=2.0):
+    """cpu_baseline leg of a variant line: the reference itself (oracle/_ref, built from the
+    reference's sources; the restatement for the detector-only RAW mode, which the
+    reference has only as tests/awgn_sweep.py's numpy receiver) on the first `nframes`
+    frames of the same batch, one host thread - its rate, and its outputs compared with the
+    GPU's for those frames (symbols, sync, cfo / time_offset bits)."""
+    import numpy as np
+
+    from oracle.pyoracle import Oracle, Reference
+
+    sf, osr, mode = r["sf"], r["osr"], r["mode"]
+    F = min(nframes, r["iq"].shape[0])
+    x = r["iq"][:F].cpu().numpy()
+    o = r["out"]
+    gs = o.symbols[:F].cpu().numpy().astype(np.int64)
+    gsync = o.sync[:F].cpu().numpy()
+    gcfo = o.cfo[:F].cpu().numpy().view(np.uint32)
+    gto = o.time_offset[:F].cpu().numpy().view(np.uint32)
+    hann = r["window"] == "hann"
+    use_ref = Reference.available() and mode != "raw"
+    impl = Reference() if use_ref else Oracle()
+    orc = Oracle()
+    bad = 0
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        for f in range(F):
+            if mode == "legacy":
+                syms, sync, cfo, toff = impl.lora_demodulate(orc.dechirp(x[f], sf, osr), sf, osr, hann)
+            elif mode == "api":
+                _, syms, sync, cfo, toff = impl.api_demodulate(x[f], sf, osr, hann)
+            else:
+                syms, sync, cfo, toff = impl.raw_demod(x[f], sf, osr, hann, dechirp=True), 0, 0.0, 0.0
+            if reps == 0:
+                ok = (np.array_equal(np.asarray(syms, np.int64), gs[f][:len(syms)]) and len(syms) == gs.shape[1]
+                      and int(sync) == int(gsync[f]) and np.float32(cfo).view(np.uint32) == gcfo[f]
+                      and np.float32(toff).view(np.uint32) == gto[f])
+                bad += not ok
+        reps += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    per = gs.shape[1]
+    what = {"legacy": "lora_demodulate after the caller's dechirp", "api": "phy::demodulate",
+            "raw": "detector per symbol"}[mode]
+    return {"value": reps * F * per / dt / 1e6, "unit": "Msymbols/s", "cores": 1,
+            "kind": "reference" if use_ref else "port",
+            "sample": f"first {F} frames of this line's batch x {reps} passes, {what}, 1 thread, {dt:.2f} s",
+            "parity_ok": bad == 0, "frames_compared": F, "frames_mismatched": bad}
 
 
 def run_channels(frames, data_syms, steps, warmup, dist, device, rank, chunk_bytes=8e9):
@@ -337,15 +434,55 @@ def run_channels(frames, data_syms, steps, warmup, dist, device, rank, chunk_byt
     bad = 0
     for (c0, n), o in zip(chunks, outs):
         bad += int((o.symbols.to(torch.int16) != tx[c0:c0 + n]).sum())
-    del iq, tx
+    # parity: every chunk against the three-launch exact path (all outputs, every frame)
+    with amd.spec_pipeline(False):
+        xplan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=True, mode="legacy", device=device)
+    pbad = 0
+    for (c0, n), o in zip(chunks, outs):
+        pr = exact_parity({"out": o}, device, xplan.run(iq[c0:c0 + n]))
+        pbad += pr["frames_mismatched"]
+    del xplan, iq, tx
     return {"frames_per_gpu": frames, "data_symbols_per_frame": data_syms, "iq_gb_per_gpu": frames * L * 8 / 1e9,
             "chunks": len(chunks), "ms_per_step": wall * 1e3 / steps,
             "ms_per_step_max_rank": wall_max * 1e3 / steps,
             "value_all_ranks_msym_s": units / wall_max / 1e6,
-            "symbols_ok_all_frames": bad == 0, "symbol_mismatches": bad}
+            "symbols_ok_all_frames": bad == 0, "symbol_mismatches": bad,
+            "parity": {"parity_ok": pbad == 0, "frames_compared": frames, "frames_mismatched": pbad,
+                       "vs": "three-launch exact path, every chunk (LORA_MI355X_SPEC=0; oracle-pinned by the GPU "
+                             "tests)"}}
 
 
-def run_modulator(sf, frames, data_syms, device, reps=3):
+def modulator_reference_leg(sf, syms16, out, nframes=8, budget_s=2.0):
+    """cpu_baseline leg of a modulator line: the reference's lora_modulate (oracle/_ref;
+    the restatement if absent) on the first frames' symbols, one thread, and every sample
+    of those frames compared with the GPU's bit for bit."""
+    import numpy as np
+
+    from oracle.pyoracle import Oracle, Reference
+
+    impl = Reference() if Reference.available() else Oracle()
+    F = min(nframes, syms16.shape[0])
+    sy = syms16[:F].cpu().numpy().astype(np.uint16)
+    g = out[:F].cpu().numpy()
+    bad = 0
+    reps = 0
+    t0 = time.perf_counter()
+    while True:
+        for f in range(F):
+            ref = impl.lora_modulate(sy[f], sf, 1, 125000, 1.0, SYNC)
+            if reps == 0:
+                bad += not np.array_equal(ref.view(np.uint32), g[f].view(np.uint32))
+        reps += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": reps * F * (sy.shape[1] + 2) / dt / 1e6, "unit": "Msymbols/s (chirps)", "cores": 1,
+            "kind": "reference" if isinstance(impl, Reference) else "port",
+            "sample": f"lora_modulate of the first {F} frames x {reps} passes, 1 thread, {dt:.2f} s",
+            "parity_ok": bad == 0, "frames_compared": F, "frames_mismatched": bad}
+
+
+def run_modulator(sf, frames, data_syms, device, reps=3, with_cpu=True):
     """lora_mod_batch throughput: samples written per second and the
     HBM write rate (8 B per sample written, symbol reads negligible)."""
     import torch
@@ -368,9 +505,16 @@ def run_modulator(sf, frames, data_syms, device, reps=3):
     torch.cuda.synchronize(device)
     ms = e0.elapsed_time(e1) / reps
     nbytes = out.numel() * 8
+    cpu = None
+    if with_cpu:
+        try:
+            cpu = modulator_reference_leg(sf, syms16, out)
+        except Exception as e:  # the CPU leg must not kill the GPU measurement
+            log("modulator cpu leg failed:", e)
     del out
     torch.cuda.empty_cache()
     return {"sf": sf, "frames": frames, "symbols_per_frame": data_syms + 2, "ms_per_call": ms,
+            "cpu_baseline": cpu,
             "msym_s": frames * (data_syms + 2) / (ms * 1e-3) / 1e6, "write_gbs": nbytes / (ms * 1e-3) / 1e9,
             "roofline_frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_written": nbytes}
 
@@ -400,7 +544,7 @@ def host_cores():
     return {"sched_getaffinity": aff, "cgroup_quota_cpus": quota, "used": used}
 
 
-def cpu_baseline(sf, iq_dev, data_syms, max_frames, time_budget_s=10.0):
+def cpu_baseline(sf, iq_dev, data_syms, max_frames, time_budget_s=10.0, gpu_out=None):
     """The reference's own lora_demodulate (oracle/_ref, compiled from the reference's
     sources, travels with the snapshot) on every usable host core (host_cores) over a
     bounded sample of the same frames; the restatement (oracle/lora_oracle.cpp) if the
@@ -430,30 +574,50 @@ def cpu_baseline(sf, iq_dev, data_syms, max_frames, time_budget_s=10.0):
         dt = time.perf_counter() - t0
         return done * data_syms / dt / 1e6, done, dt
 
+    parity = None
+    if gpu_out is not None:
+        # the reference's outputs on the sample against the GPU run's for the same frames
+        import numpy as np
+
+        rs, rsync, rcfo, rtoff, _ = impl.demod_frames(x, sf, 1, False, dechirp=True, threads=threads)
+        gs = gpu_out.symbols[:F].cpu().numpy().astype(np.int64)
+        bad = ((rs[:, :gs.shape[1]].astype(np.int64) != gs).any(1) | (rsync != gpu_out.sync[:F].cpu().numpy())
+               | (rcfo.view(np.uint32) != gpu_out.cfo[:F].cpu().numpy().view(np.uint32))
+               | (rtoff.view(np.uint32) != gpu_out.time_offset[:F].cpu().numpy().view(np.uint32)))
+        parity = {"parity_ok": not bool(bad.any()), "frames_compared": F, "frames_mismatched": int(bad.sum()),
+                  "vs": kind + " outputs on the sample frames (symbols, sync, cfo / time_offset bits)"}
     all_rate, done, dt = rate(x, threads, True, time_budget_s)
     one_rate, _, _ = rate(x[: max(1, min(F, 4))], 1, True, time_budget_s / 3)
     xd = Oracle().dechirp(x.reshape(-1), sf).reshape(x.shape)  # same fp32 products as the caller loop
     demod_only, _, _ = rate(xd, threads, False, time_budget_s / 3)
     return {"value": all_rate, "unit": "Msymbols/s", "cores": threads, "kind": kind,
             "host_cores": cores, "single_core": one_rate, "demod_only_all_cores": demod_only,
+            "reference_parity": parity,
             "cpu_model": _cpu_model(),
             "sample": f"{done} frames of the SF{sf} bench batch ({data_syms}+2 symbols each, {F} distinct), "
                       f"caller-side dechirp + {what}, {threads} threads, {dt:.2f} s; single_core: same on 1 "
                       f"thread; demod_only: input dechirped beforehand"}
 
 
-def fast_summary(r):
+def fast_summary(r, exact):
     """LORA_PRECISION_FAST line (hardware sin/cos rotation; stated tolerance in
-    include/lora_mi355x.h): same workload and inputs as the exact run."""
+    include/lora_mi355x.h): same workload and inputs as the exact run, whose symbols it is
+    compared with (a tolerance mode: agreement is reported, not required)."""
+    import torch
+
+    agree = float((r["out"].symbols.to(torch.int32) == exact["out"].symbols.to(torch.int32)).float().mean())
     return {"precision": "fast", "ms_per_step": r["ms_per_step"], "stage_ms": r["stage_ms"],
+            "parity": {"tolerance_mode": True, "symbol_agreement_with_exact": agree},
             "symbols_ok": r["symbols_ok"], "value_all_ranks_msym_s": r["msym_s_all_ranks"],
             "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS}
 
 
-def variant_summary(r, base, note):
+def variant_summary(r, base, note, parity=None):
     """A data-dependent variant of a workload: `ratio_to_headline` is its time per data
-    symbol over the headline's (> 1 = slower)."""
-    return {"note": note, "frames": r["frames"], "data_symbols_per_frame": r["data_symbols"] // r["frames"],
+    symbol over the headline's (> 1 = slower); `parity` measured in the run
+    (exact_parity / reference_leg)."""
+    return {"note": note, "parity": parity, "frames": r["frames"],
+            "data_symbols_per_frame": r["data_symbols"] // r["frames"],
             "ms_per_step": r["ms_per_step"], "stage_ms": r["stage_ms"],
             "value_all_ranks_msym_s": r["msym_s_all_ranks"], "ser_vs_tx": r["ser_vs_tx"],
             "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS, "kernels": r["kernels"],
@@ -500,7 +664,9 @@ def roofline(r, probe=None):
     """roofline object for one workload: the dominant kernel (HIP-event time, algorithmic
     bytes per launch) and the whole step (pipeline_frac); counter bytes from the
     committed rocprofv3 profile (profiles/pmc_summary.json, labelled as such)."""
-    wl = "sf%d" % r["sf"]
+    # the committed counter profile of this workload: sf7 / sf12 (the headline shapes), or
+    # <mode>_sf7 for the API / RAW lines
+    wl = ("sf%d" % r["sf"]) if r.get("mode", "legacy") == "legacy" else "%s_sf%d" % (r["mode"], r["sf"])
     pmc_step = load_pmc(wl, "hbm_bytes_per_step")
     pmc_dom = load_pmc(wl, "hbm_bytes_per_launch")
     return {"bound": "hbm", "kernel": r["dominant_kernel"],
@@ -579,11 +745,17 @@ def main():
             print(json.dumps(public(r12)))
         return
     r7 = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank)
+    r7["parity"] = exact_parity(r7, device)
+    probe = None
+    try:
+        probe = hbm_probe(device)
+    except Exception as e:  # a probe must not kill the measurement
+        log("hbm probe failed:", e)
     extra = {}
     if not args.no_fast:
         r7f = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device,
                          precision="fast", inputs=(r7["syms"], r7["iq"]), rank=rank)
-        extra["fast_rotation_sf7"] = fast_summary(r7f)
+        extra["fast_rotation_sf7"] = fast_summary(r7f, r7)
         del r7f
     if not args.no_variants:
         # data-dependent slow rotation path: sync nibbles 0xF -> estimated cfo ~0.94 ->
@@ -592,30 +764,35 @@ def main():
                          rank=rank)
         extra["sync_ff_sf7"] = variant_summary(rff, r7, "sync 0xFF: large estimated CFO, Payne-Hanek "
                                                         "reduction in the rotation (ser_vs_tx is the reference's "
-                                                        "own CFO-shift behaviour, not an error)")
+                                                        "own CFO-shift behaviour, not an error)",
+                                               exact_parity(rff, device))
         del rff
         rn = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, snr_db=0.0,
                         rank=rank)
         extra["awgn_0db_sf7"] = variant_summary(rn, r7, "AWGN 0 dB (sigma/sqrt2 per component, "
-                                                       "awgn_sweep_gtest.cpp:76-80); t_off != 0 frames")
+                                                       "awgn_sweep_gtest.cpp:76-80); t_off != 0 frames",
+                                                exact_parity(rn, device))
         del rn
         # the certified pipeline's worst case: near-ties at low SNR are recomputed exactly
         rn = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, snr_db=-10.0,
                         rank=rank)
         extra["awgn_m10db_sf7"] = variant_summary(rn, r7, "AWGN -10 dB: symbol errors and near-ties; symbols "
-                                                         "failing certification are recomputed exactly")
+                                                         "failing certification are recomputed exactly",
+                                                  exact_parity(rn, device))
         del rn
         # the Hann window (LoRaDemod.cpp:158-160) on the headline batch
         rh = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, window="hann",
                         inputs=(r7["syms"], r7["iq"]), rank=rank)
         extra["hann_sf7"] = variant_summary(rh, r7, "Hann window, same batch (ser_vs_tx: the window's own "
-                                                    "effect on the reference's decisions, not an error)")
+                                                    "effect on the reference's decisions, not an error)",
+                                            exact_parity(rh, device))
         del rh
         # a 255-byte payload: 510 data symbols per frame (lora_encode: 2 symbols per byte)
         long_frames = max(1, args.frames * args.data_symbols // 510)
         rl = run_config(7, long_frames, 510, args.steps, args.warmup, dist, device, rank=rank)
         extra["long_frames_sf7"] = variant_summary(rl, r7, "255-byte payload: 2 + 510 symbols per frame, "
-                                                          "noiseless, same data symbols per step")
+                                                          "noiseless, same data symbols per step",
+                                                   exact_parity(rl, device))
         del rl
         torch.cuda.empty_cache()
         # oversampled LEGACY frames (osr 2: gr_lora_sdr_interop.cpp:34's capture shape; osr 4):
@@ -624,17 +801,20 @@ def main():
         for osr in (2, 4):
             ro = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank,
                             osr=osr)
-            line = variant_summary(ro, r7, f"osr {osr}: {osr} x the IQ bytes per symbol, same data symbols")
+            rt = None
+            if osr == 2:
+                rt = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank,
+                                osr=osr, inputs=(ro["syms"], ro["iq"]), spec=False)
+            line = variant_summary(ro, r7, f"osr {osr}: {osr} x the IQ bytes per symbol, same data symbols",
+                                   exact_parity(ro, device, rt["out"] if rt is not None else None))
             line["symbol_pass_gbs"] = ro["dominant_gbs"]
             line["symbol_pass_frac"] = ro["dominant_gbs"] / HBM_PEAK_GBS
             line["step_bytes"] = ro["step_bytes"]
             # HBM bytes the counters saw per symbol-pass launch over its algorithmic bytes
-            # (committed rocprofv3 FETCH_SIZE / WRITE_SIZE profile, tools/pmc_r04.py)
+            # (committed rocprofv3 FETCH_SIZE / WRITE_SIZE profile, tools/pmc_r05.py)
             line["symbol_pass_counter_over_algorithmic"] = load_pmc(f"osr{osr}_sf7", "traffic_over_algorithmic")
             line["step_counter_over_algorithmic"] = load_pmc(f"osr{osr}_sf7", "step_traffic_over_algorithmic")
-            if osr == 2:
-                rt = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank,
-                                osr=osr, inputs=(ro["syms"], ro["iq"]), spec=False)
+            if rt is not None:
                 line["three_launch"] = {"ms_per_step": rt["ms_per_step"], "stage_ms": rt["stage_ms"],
                                         "pipeline_frac": rt["pipeline_gbs"] / HBM_PEAK_GBS,
                                         "symbols_ok": rt["symbols_ok"], "kernels": rt["kernels"]}
@@ -642,22 +822,46 @@ def main():
             extra[f"osr{osr}_sf7"] = line
             del ro
             torch.cuda.empty_cache()
-        extra["mod_sf7"] = run_modulator(7, args.frames, args.data_symbols, device)
+        # the reference's two other receivers on the headline's shape: the workspace API's
+        # demodulate (phy.cpp:178-239, rx_runner's path: estimate on raw samples, fused
+        # per-symbol down-chirp) and the detector alone (tests/awgn_sweep.py:262-273); each
+        # with its own roofline and a reference leg (rate + parity on a 32-frame sample)
+        for mode, note in (("api", "workspace API demodulate (phy.cpp:178-239) on raw modulated frames; "
+                                   "ser_vs_tx is the reference's own estimate-on-raw-samples behaviour"),
+                           ("raw", "detector only per symbol (awgn_sweep.py:262-273), all 66 symbols an output")):
+            rm = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank,
+                            mode=mode, inputs=(r7["syms"], r7["iq"]))
+            leg = None
+            if rank == 0 and world == 1 and not args.no_cpu:
+                try:
+                    leg = reference_leg(rm)
+                except Exception as e:  # the CPU leg must not kill the GPU measurement
+                    log(f"{mode} reference leg failed:", e)
+            line = variant_summary(rm, r7, note, {"parity_ok": leg["parity_ok"] if leg else None,
+                                                  "vs": "cpu_baseline leg (reference outputs on its sample)"})
+            line["roofline"] = roofline(rm, probe)
+            line["cpu_baseline"] = leg
+            extra[f"{mode}_sf7"] = line
+            del rm
+        extra["mod_sf7"] = run_modulator(7, args.frames, args.data_symbols, device,
+                                         with_cpu=rank == 0 and not args.no_cpu)
     r12 = None
     if not args.no_sf12:
         r12 = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2),
                          args.warmup, dist, device, rank=rank)
         extra["sf12"] = public(r12)
         extra["sf12"]["value_all_ranks_msym_s"] = r12["msym_s_all_ranks"]
-        extra["sf12"]["roofline"] = roofline(r12)
+        extra["sf12"]["roofline"] = roofline(r12, probe)
+        extra["sf12"]["parity"] = exact_parity(r12, device)
         if not args.no_fast:
             r12f = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 2, 2), args.warmup,
                               dist, device, precision="fast", inputs=(r12["syms"], r12["iq"]), rank=rank)
-            extra["fast_rotation_sf12"] = fast_summary(r12f)
+            extra["fast_rotation_sf12"] = fast_summary(r12f, r12)
             del r12f
         if rank == 0 and not args.no_cpu and world == 1:
             try:
-                extra["sf12"]["cpu_baseline"] = cpu_baseline(12, r12["iq"], args.data_symbols, 64)
+                extra["sf12"]["cpu_baseline"] = cpu_baseline(12, r12["iq"], args.data_symbols, 64,
+                                                             gpu_out=r12["out"])
             except Exception as e:  # the CPU leg must not kill the GPU measurement
                 log("sf12 cpu baseline failed:", e)
         if not args.no_variants:
@@ -671,7 +875,8 @@ def main():
             r12n = run_config(12, args.sf12_frames, args.data_symbols, max(args.steps // 4, 2), args.warmup,
                               dist, device, inputs=(r12["syms"], iqn), rank=rank)
             extra["awgn_m10db_sf12"] = variant_summary(r12n, r12, "AWGN -10 dB on the SF12 batch: symbol errors "
-                                                                  "and near-ties, recomputed exactly")
+                                                                  "and near-ties, recomputed exactly",
+                                                       exact_parity(r12n, device))
             del r12n
         del r12
         torch.cuda.empty_cache()
@@ -679,19 +884,15 @@ def main():
             # the SF12 batch's shape (15,625 frames): the modulator's time is set by each
             # frame's sequential phase chain (k_mod_phase), so a smaller batch only measures
             # that chain's length
-            extra["mod_sf12"] = run_modulator(12, args.sf12_frames, args.data_symbols, device)
+            extra["mod_sf12"] = run_modulator(12, args.sf12_frames, args.data_symbols, device,
+                                              with_cpu=rank == 0 and not args.no_cpu)
     if not args.no_channels:
         extra["channels"] = run_channels(args.channel_frames, 16, max(args.steps // 4, 2), 1, dist, device, rank)
         torch.cuda.empty_cache()
-    probe = None
-    try:
-        probe = hbm_probe(device)
-    except Exception as e:  # a probe must not kill the measurement
-        log("hbm probe failed:", e)
     cpu = None
     if rank == 0 and not args.no_cpu and world == 1:
         try:
-            cpu = cpu_baseline(7, r7["iq"], args.data_symbols, 4000)
+            cpu = cpu_baseline(7, r7["iq"], args.data_symbols, 4000, gpu_out=r7["out"])
         except Exception as e:  # the CPU leg must not kill the GPU measurement
             log("cpu baseline failed:", e)
     if rank == 0:
@@ -713,7 +914,8 @@ def main():
             "config": {"workload": workload, "launch": LAUNCH, "sf": 7, "bw_hz": 125000, "osr": 1,
                        "frames_per_gpu": args.frames, "data_symbols_per_frame": args.data_symbols,
                        "parallelism": f"frames sharded x{world}, no collective (gloo timing only)",
-                       "ranks": ranks, "symbols_ok": r7["symbols_ok"], "stage_ms": r7["stage_ms"],
+                       "ranks": ranks, "symbols_ok": r7["symbols_ok"], "parity": r7["parity"],
+                       "stage_ms": r7["stage_ms"],
                        "kernels": r7["kernels"], "spec_recomputed_per_step": r7["spec_recomputed_per_step"],
                        "msym_s_all_symbols": r7["msym_s_all"] * world,
                        "pipeline_gbs_per_gpu": r7["pipeline_gbs"]},

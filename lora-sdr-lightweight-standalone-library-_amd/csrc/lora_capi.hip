@@ -552,6 +552,19 @@ __device__ __forceinline__ float chirp_f0(const ModArgs& a, int64_t frame, int c
   return (2.0f * PI_F * (float)(int)v * a.bw_scale) / ((float)a.N * (float)a.osr);
 }
 
+// glibc sincosf of one sample per lane, the reduction chosen per wave: the fast one when
+// every active lane's |y| < 120, the Payne-Hanek one when every |y| is in [120, inf) (an
+// SF12 chirp's phases, mid-chirp), else both evaluated and selected (lm_sincosf_bf).  The
+// results are lm_sincosf's in every case (tests/native/libm_check: each form vs glibc).
+__device__ __forceinline__ void mod_sincosf(float y, float* s, float* c) {
+  if (__all(lm_sincosf_fast_ok(y)))
+    lm_sincosf_fast(y, s, c);
+  else if (__all(lm_sincosf_large_ok(y)))
+    lm_sincosf_large(y, s, c);
+  else
+    lm_sincosf_bf(y, s, c);
+}
+
 // K steps of the genChirp recurrence (ChirpGenerator.hpp:118-128: f += fStep, wrap at
 // fMax, phase += f, all fp32), speculatively without the wrap: fStep > 0, so f only grows
 // between wraps and the K unwrapped steps are the recurrence's own exactly when the last
@@ -661,7 +674,7 @@ __global__ void __launch_bounds__(kModLanes * kModWaves) k_mod_samples(ModArgs a
     if (j < cnt) {
       for (int ch = sub; ch < nvalid; ch += kModLanes / kModBatch) {
         float sn, cs;
-        lm_sincosf_bf(tile[ch][j], &sn, &cs);
+        mod_sincosf(tile[ch][j], &sn, &cs);
         a.iq[(w0 + ch) * a.step + i0 + j] = cf{a.ampl * cs, a.ampl * sn};
       }
     }
@@ -827,7 +840,7 @@ __global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int 
     const float* b = buf[t % 3];
     for (int i = wk; i < n; i += nwk) {
       float sn, cs;
-      lm_sincosf_bf(b[i], &sn, &cs);
+      mod_sincosf(b[i], &sn, &cs);
       out[s0 + i] = cf{a.ampl * cs, a.ampl * sn};
     }
   };

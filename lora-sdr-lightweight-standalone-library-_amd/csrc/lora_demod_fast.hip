@@ -912,10 +912,22 @@ template <int SF>
 constexpr size_t spec_dtl_offset() {
   return (((size_t)Geo<SF>::SPW * lds_row<SF>() + demod_twl_entries<SF, true>()) * sizeof(cf) + 15) & ~(size_t)15;
 }
+// SF 6-8: instead of the table-phase-0 slice, the whole doubled dechirp table (KArgs::down,
+// 2N entries: 1-4 KB), so a window at any table phase - every frame with t_off != 0, i.e.
+// every captured frame - reads its table values from LDS too (four workgroups per CU still
+// fit); SF9 keeps the slice (its 8 KB table would cost the fourth workgroup).
+#ifndef LORA_DTAB
+#define LORA_DTAB 1
+#endif
+template <int SF>
+constexpr bool spec_dtab() {
+  return LORA_DTAB && Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2 &&
+         4 * (spec_dtl_offset<SF>() + 2 * sizeof(cf) * Geo<SF>::N) <= 160 * 1024;
+}
 template <int SF>
 constexpr size_t spec_lds_bytes() {
   constexpr bool pf2 = Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2;
-  return pf2 ? spec_dtl_offset<SF>() + 16 * 8 * Geo<SF>::T
+  return pf2 ? spec_dtl_offset<SF>() + (spec_dtab<SF>() ? 2 * sizeof(cf) * Geo<SF>::N : 16 * 8 * Geo<SF>::T)
              : sizeof(cf) * ((size_t)Geo<SF>::SPW * lds_row<SF>() + demod_twl_entries<SF, true>());
 }
 
@@ -1057,11 +1069,16 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   // (PF geometries, MODE 0) the dechirp table's pairs at table phase 0 - what every window
   // of a t_off = 0 frame reads - staged after the twiddles: dtl[p T + c] = downP[p (N + T) + c]
   constexpr bool DTL = WL && G::NPASS == 2 && !OSRN && MODE == 0;
+  // DTAB (SF 6-8): the whole doubled table instead, for every table phase
+  constexpr bool DTAB = DTL && spec_dtab<SF>();
   float4* dtl = reinterpret_cast<float4*>(smem + spec_dtl_offset<SF>());
+  cf* dtab = reinterpret_cast<cf*>(smem + spec_dtl_offset<SF>());
   if constexpr (NTW > 0) {
     const int tid = threadIdx.x;
     if (tid < NTW) twl[tid] = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
-    if constexpr (DTL) {
+    if constexpr (DTAB) {
+      for (int i = tid; i < 2 * N; i += 256) dtab[i] = a.down[i];
+    } else if constexpr (DTL) {
       static_assert(8 * T <= 256, "one staged pair per thread");
       if (tid < 8 * T) dtl[tid] = reinterpret_cast<const float4*>(a.downP)[(tid / T) * (N + T) + tid % T];
     }
@@ -1318,12 +1335,22 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
         const __amdgpu_buffer_rsrc_t rd =
             __builtin_amdgcn_make_buffer_rsrc((void*)a.downP, (short)0, 0x7fffffff, 0x00020000);
         const int vt = (B.cg + lr) * 16;
+        if constexpr (DTAB) {
+          // any table phase from the staged table: down[cg + lr + T q], two per ds_read2_b64
+          const cf* dq = dtab + B.cg + lr;
+#pragma unroll
+          for (int pp = 0; pp < P / 2; ++pp) {
+            const cf d0 = dq[2 * pp * T], d1 = dq[(2 * pp + 1) * T];
+            dt[pp] = float4{d0.re, d0.im, d1.re, d1.im};
+          }
+        } else {
         // every window of the wave at table phase 0 (t_off = 0 frames): the LDS slice
         const bool cg0 = __builtin_amdgcn_readfirstlane(__ballot(B.cg != 0) == 0);
 #pragma unroll
         for (int pp = 0; pp < P / 2; ++pp)
           dt[pp] = cg0 ? dtl[pp * T + lr]
                        : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vt, pp * (N + T) * 16, 0));
+        }
       }
 
       // select (a misaligned window), dechirp, window max

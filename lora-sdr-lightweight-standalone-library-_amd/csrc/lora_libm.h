@@ -346,6 +346,37 @@ LM_FN void lm_sincosf_bf(float y, float* sinp, float* cosp) {
 // True when lm_sincosf_fast is exact for y.
 LM_FN int lm_sincosf_fast_ok(float y) { return lm_abstop12(y) < 0x42fu; }
 
+// lm_sincosf_bf's large-argument branch alone: exact for finite |y| >= 120
+// (lm_sincosf_large_ok), where glibc takes reduce_large - the same integer Payne-Hanek
+// reduction and polynomial, without evaluating reduce_fast and selecting.
+LM_FN int lm_sincosf_large_ok(float y) {
+  const uint32_t top = lm_abstop12(y);
+  return top >= 0x42fu && top < 0x7f8u;
+}
+LM_FN void lm_sincosf_large(float y, float* sinp, float* cosp) {
+  uint32_t xi = lm_asuint(y);
+  const int sign = (int)(xi >> 31);
+  const uint32_t* arr = &LM_INV_PIO4[(xi >> 26) & 15];
+  const int shift = (xi >> 23) & 7;
+  xi = (xi & 0xffffffu) | 0x800000u;
+  xi <<= shift;
+  uint64_t res0 = (uint64_t)(uint32_t)(xi * arr[0]);
+  const uint64_t res1 = (uint64_t)xi * arr[4];
+  const uint64_t res2 = (uint64_t)xi * arr[8];
+  res0 = (res2 >> 32) | (res0 << 32);
+  res0 += res1;
+  const uint64_t nn = (res0 + (1ull << 61)) >> 62;
+  res0 -= nn << 62;
+  const double xr = (double)(int64_t)res0 * LM_PI63;
+  const int n = (int)nn;
+  const int nq = (int)nn + sign;
+  const double xs = ((nq ^ (nq >> 1)) & 1) ? -xr : xr;
+  float sv, cv;
+  lm_sincosf_poly(xs, xr * xr, (nq & 2) != 0, &sv, &cv);
+  *sinp = (n & 1) ? cv : sv;
+  *cosp = (n & 1) ? sv : cv;
+}
+
 // ---------------------------------------------------------------------------
 // hypotf (glibc 2.35): exact double sum of squares, double sqrt, round to float.
 // ---------------------------------------------------------------------------

@@ -28,10 +28,10 @@ static bool same(float a, float b) { return bits(a) == bits(b) || (isnan(a) && i
 int main(int argc, char** argv) {
   const uint64_t stride = argc > 1 ? strtoull(argv[1], 0, 10) : 97;
   const int T = argc > 2 ? atoi(argv[2]) : 4;
-  std::atomic<uint64_t> n_sc{0}, bad_sc{0}, n_fast{0}, bad_fast{0}, bad_fastk{0}, bad_nz{0}, bad_bf{0};
+  std::atomic<uint64_t> n_sc{0}, bad_sc{0}, n_fast{0}, bad_fast{0}, bad_fastk{0}, bad_nz{0}, bad_bf{0}, n_lg{0}, bad_lgr{0};
   std::atomic<uint64_t> n_o{0}, bad_at{0}, bad_hy{0}, bad_lg{0}, bad_l10{0};
   auto work = [&](int t) {
-    uint64_t c_sc = 0, b_sc = 0, c_f = 0, b_f = 0, b_fk = 0, b_nz = 0, b_bf = 0;
+    uint64_t c_sc = 0, b_sc = 0, c_f = 0, b_f = 0, b_fk = 0, b_nz = 0, b_bf = 0, c_lg = 0, b_lgr = 0;
     for (uint64_t u = (uint64_t)t * stride; u < (1ull << 32); u += (uint64_t)T * stride) {
       const float y = flt((uint32_t)u);
       float s, c, s2, c2;
@@ -41,6 +41,11 @@ int main(int argc, char** argv) {
       if (!same(s, s2) || !same(c, c2)) ++b_sc;
       lm_sincosf_bf(y, &s2, &c2);
       if (!same(s, s2) || !same(c, c2)) ++b_bf;
+      if (lm_sincosf_large_ok(y)) {
+        ++c_lg;
+        lm_sincosf_large(y, &s2, &c2);
+        if (!same(s, s2) || !same(c, c2)) ++b_lgr;
+      }
       if (lm_sincosf_fast_ok(y)) {
         ++c_f;
         lm_sincosf_fast(y, &s2, &c2);
@@ -56,6 +61,8 @@ int main(int argc, char** argv) {
     }
     n_sc += c_sc; bad_sc += b_sc; n_fast += c_f; bad_fast += b_f; bad_fastk += b_fk; bad_nz += b_nz;
     bad_bf += b_bf;
+    n_lg += c_lg;
+    bad_lgr += b_lgr;
     uint64_t c_o = 0, b_a = 0, b_h = 0, b_l = 0, b_10 = 0;
     for (uint64_t i = t; i < 4000000; i += T) {
       const uint64_t h = mix(i * 0x9e3779b97f4a7c15ull + 12345);
@@ -73,6 +80,7 @@ int main(int argc, char** argv) {
   for (auto& x : th) x.join();
   printf("sincosf %llu %llu\n", (unsigned long long)n_sc, (unsigned long long)bad_sc);
   printf("sincosf_bf %llu %llu\n", (unsigned long long)n_sc, (unsigned long long)bad_bf);
+  printf("sincosf_large %llu %llu\n", (unsigned long long)n_lg, (unsigned long long)bad_lgr);
   printf("sincosf_fast %llu %llu\n", (unsigned long long)n_fast, (unsigned long long)bad_fast);
   printf("sincosf_fast_k %llu %llu\n", (unsigned long long)n_fast, (unsigned long long)bad_fastk);
   printf("sincosf_fast_k_nz %llu %llu\n", (unsigned long long)n_fast, (unsigned long long)bad_nz);

@@ -33,7 +33,7 @@ def results():
     return res
 
 
-@pytest.mark.parametrize("name", ["sincosf", "sincosf_bf", "sincosf_fast", "sincosf_fast_k", "sincosf_fast_k_nz",
+@pytest.mark.parametrize("name", ["sincosf", "sincosf_bf", "sincosf_large", "sincosf_fast", "sincosf_fast_k", "sincosf_fast_k_nz",
                                   "atan2f", "hypotf", "logf", "log10f"])
 def test_bit_exact_vs_glibc(results, name):
     n, bad = results[name]
