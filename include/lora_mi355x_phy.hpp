@@ -57,6 +57,11 @@ struct lora_demod_plan;  // lora_mi355x.h
 /* 0 when liblora_phy.so's load-time runtime is up (the legacy calls then allocate nothing),
  * else the set-up step that failed (csrc/lora_phy_dropin.hip). */
 extern "C" int lora_phy_dropin_status(void);
+/* Diagnostics: where the last lora_demodulate / lora_modulate call on the private AQL queue
+ * spent its time, in microseconds - out[0..3] the demodulation's copy into the pinned
+ * staging, host logic (lora_demod_batch with the launch recorder), dispatch to completion
+ * (aql_run), copy out; out[4..7] the same for the modulation.  Returns 8. */
+extern "C" int lora_phy_dropin_last_timing(double* out);
 
 namespace lora_phy {
 

@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -545,10 +546,18 @@ struct ModArgs {
   int64_t sym_count;
   cf* iq;
   int64_t frames;
+  // k_mod_frame: the configuration's run tables (mod_run_table), runs of chirp value v at
+  // seg[v * seg_cap], their count at cnt[v] (-1: over the cap), for v < seg_n; null: none
+  const lora::ChirpSeg* seg;
+  const int* cnt;
+  int seg_n, seg_cap;
 };
 
+__device__ __forceinline__ unsigned chirp_value(const ModArgs& a, int64_t frame, int c) {
+  return c == 0 ? a.sw0 : c == 1 ? a.sw1 : a.syms[frame * a.sym_count + (c - 2)];
+}
 __device__ __forceinline__ float chirp_f0(const ModArgs& a, int64_t frame, int c) {
-  const unsigned v = c == 0 ? a.sw0 : c == 1 ? a.sw1 : a.syms[frame * a.sym_count + (c - 2)];
+  const unsigned v = chirp_value(a, frame, c);
   return (2.0f * PI_F * (float)(int)v * a.bw_scale) / ((float)a.N * (float)a.osr);
 }
 
@@ -563,6 +572,20 @@ __device__ __forceinline__ void mod_sincosf(float y, float* s, float* c) {
     lm_sincosf_large(y, s, c);
   else
     lm_sincosf_bf(y, s, c);
+}
+
+// mod_sincosf of two samples per lane, the reduction chosen per wave for both
+__device__ __forceinline__ void mod_sincosf2(float y0, float y1, float* s, float* c) {
+  if (__all(lm_sincosf_fast_ok(y0) && lm_sincosf_fast_ok(y1))) {
+    const float y[2] = {y0, y1};
+    lm_sincosf_fast_k<2>(y, s, c);
+  } else if (__all(lm_sincosf_large_ok(y0) && lm_sincosf_large_ok(y1))) {
+    lm_sincosf_large(y0, &s[0], &c[0]);
+    lm_sincosf_large(y1, &s[1], &c[1]);
+  } else {
+    lm_sincosf_bf(y0, &s[0], &c[0]);
+    lm_sincosf_bf(y1, &s[1], &c[1]);
+  }
 }
 
 // K steps of the genChirp recurrence (ChirpGenerator.hpp:118-128: f += fStep, wrap at
@@ -688,18 +711,25 @@ __global__ void __launch_bounds__(kModLanes * kModWaves) k_mod_samples(ModArgs a
 // ---- few frames: one workgroup per frame (k_mod_frame) ------------------------------
 // With few frames the bulk kernels above leave the chip idle while one lane per frame
 // walks the whole frame's recurrence at five dependent operations per sample (SF7, one
-// frame: ~180 us).  Here a frame's samples go through windows of <= 4096 samples in a
-// three-stage pipeline over one workgroup:
+// frame: ~180 us).  Here a frame's samples go through windows of <= 2048 samples in a
+// four-stage pipeline over one workgroup:
 //   * waves 1-3 fill window t+1 with its frequencies - short chirps (< kMfTabMin samples)
 //     by one lane per chirp running the frequency recurrence, long ones from the runs of
 //     lora_chirp.h (built one window ahead by a few lanes, then evaluated in parallel);
-//   * lane 0 of wave 0 turns window t's frequencies into phases in place - the one truly
-//     sequential part, a single dependent fp32 add per sample (ChirpGenerator.hpp:121)
-//     plus the per-chirp wrap (:130);
-//   * waves 1-3 evaluate window t-1's samples (glibc-exact sincosf, :122) and store them.
+//   * lane 0 of wave 0 runs window t's phase additions (ChirpGenerator.hpp:121), the one
+//     truly sequential part - one dependent fp32 add per sample, the frequencies read two
+//     blocks ahead - and records the phase at the start of each 32-sample block (and the
+//     per-chirp wrap, :130);
+//   * waves 1-3 recompute window t-1's phases block by block from those starts (the same
+//     additions, in parallel), then evaluate window t-2's samples (glibc-exact sincosf,
+//     :122) with coalesced stores.
+// A dependent add issues every ~4.6 cycles on one wave; a DS store per sample in the chain
+// lane cost 14-15 cycles per sample (tools/micro/chain_rate.hip), hence the block starts.
 // Results are the recurrence's own, bit for bit (the runs are exact, chirp_seg_check).
-constexpr int kMfWin = 4096;     // samples per window (whole chirps, or an exact fraction of one)
-constexpr int kMfTabMin = 1024;  // chirps of at least this many samples take runs
+constexpr int kMfWin = 2048;     // samples per window (whole chirps, or an exact fraction of one)
+constexpr int kMfBlk = 32;       // samples per recorded block start
+constexpr int kMfPad = 2 * kMfBlk;  // the chain's read-ahead past a window
+constexpr int kMfTabMin = 512;   // chirps of at least this many samples take runs
 constexpr int kMfTabChirps = kMfWin / kMfTabMin;  // long chirps per window
 constexpr int kMfSegMax = 92;    // runs per chirp: lora::chirp_seg_cap(12)
 static_assert(kMfSegMax >= lora::chirp_seg_cap(12), "run table per chirp");
@@ -707,12 +737,30 @@ constexpr int kMfThreads = 256;
 constexpr int kMfWorkers = kMfThreads - 64;
 constexpr int64_t kMfMaxFrames = 512;  // at most this many frames take k_mod_frame
 
+// The runs of every chirp value v < n of one configuration (one lane per value), for
+// k_mod_frame's long chirps: built once per (device, sf, osr, bandwidth) by mod_run_table,
+// so the frame kernel copies a chirp's table instead of deriving it (one lane, ~650 cycles
+// per run: 44 k cycles per SF12 chirp - more than the chirp's whole phase chain).
+__global__ void __launch_bounds__(64) k_mod_runs(ModArgs a, int n, int cap, lora::ChirpSeg* seg, int* cnt) {
+  const int v = blockIdx.x * 64 + threadIdx.x;
+  if (v >= n) return;
+  const lora::ChirpConst cc{a.fMin, a.fMax, a.fStep, a.fMax - a.fMin};
+  const float f0 = (2.0f * PI_F * (float)v * a.bw_scale) / ((float)a.N * (float)a.osr);  // chirp_f0's
+  cnt[v] = lora::chirp_segments(a.fMin + f0, a.step, cc, seg + (size_t)v * cap, cap);
+}
+
 // window t's table group: a window of whole chirps is its own group, the windows of one
 // long chirp share the chirp's
 __device__ __forceinline__ int mf_group(int t, int W, int step) { return step <= W ? t : (int)((int64_t)t * W / step); }
 
+// ChirpGenerator.hpp:130, after a chirp's last sample
+__device__ __forceinline__ float mf_wrap(float phase) {
+  return (float)((double)phase - floor((double)phase / (2 * M_PI)) * 2 * M_PI);
+}
+
 __global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int nwin) {
-  __shared__ __attribute__((aligned(16))) float buf[3][kMfWin];
+  __shared__ __attribute__((aligned(16))) float buf[4][kMfWin + kMfPad];
+  __shared__ float pst[4][kMfWin / kMfBlk];  // phase before each block's first sample
   __shared__ lora::ChirpSeg tab[2][kMfTabChirps][kMfSegMax];
   __shared__ int tcnt[2][kMfTabChirps];
   const int64_t fr = blockIdx.x;
@@ -727,6 +775,7 @@ __global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int 
   // workers (the others fill and evaluate meanwhile)
   const int nbuild = runs ? (a.step <= W ? W / a.step : 1) : 0;
   const int nwk = kMfWorkers - nbuild;  // workers that fill and evaluate
+  auto wlen = [&](int t) { return (int)min((int64_t)W, total - (int64_t)t * W); };
   auto build = [&](int t) {
     const int j = wk - nwk;
     if (!runs || j < 0 || t >= nwin) return;
@@ -735,22 +784,51 @@ __global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int 
     const int c = (int)(s0 / a.step) + j;
     if (c >= a.nchirp || (int64_t)c * a.step >= s0 + W) return;
     const int slot = mf_group(t, W, a.step) & 1;
-    tcnt[slot][j] = lora::chirp_segments(a.fMin + chirp_f0(a, fr, c), a.step, cc, tab[slot][j], cap);
+    const unsigned v = chirp_value(a, fr, c);
+    if (a.seg && (int)v < a.seg_n) {
+      // the precomputed runs of this chirp value (mod_run_table): a copy, 16 bytes per load
+      const int nr = a.cnt[v];
+      tcnt[slot][j] = nr;
+      const uint4* src = reinterpret_cast<const uint4*>(a.seg + (size_t)v * a.seg_cap);
+      uint4* dst = reinterpret_cast<uint4*>(tab[slot][j]);
+      for (int r = 0; r < nr; ++r) dst[r] = src[r];
+    } else {
+      tcnt[slot][j] = lora::chirp_segments(a.fMin + chirp_f0(a, fr, c), a.step, cc, tab[slot][j], cap);
+    }
   };
-  // window t's frequencies into buf[t % 3]
+  // window t's frequencies into buf[t % 4]
   auto fill = [&](int t) {
     if (wk < 0 || wk >= nwk || t >= nwin) return;
     const int64_t s0 = (int64_t)t * W;
-    const int n = (int)min((int64_t)W, total - s0);
-    float* b = buf[t % 3];
+    const int n = wlen(t);
+    float* b = buf[t % 4];
     if (!runs) {
       // whole short chirps, one lane each: the recurrence itself
+      // (four values per store: a DS store reads its data after issue, so one store per step
+      // made each step wait for the previous store)
+      // (and two quads per round in registers of their own: a quad's registers are rewritten
+      // only after the other quad's store has been issued)
       for (int c = wk; c < n / a.step; c += nwk) {
         float f = a.fMin + chirp_f0(a, fr, (int)(s0 / a.step) + c);
-        float* bc = b + c * a.step;
-        for (int k = 0; k < a.step; ++k) {
-          f = lora::chirp_fstep(f, cc);
-          bc[k] = f;
+        float4* bc = reinterpret_cast<float4*>(b + c * a.step);  // step % 4 == 0, 16-byte aligned
+        auto quad = [&](float4& v) {
+          v.x = f = lora::chirp_fstep(f, cc);
+          v.y = f = lora::chirp_fstep(f, cc);
+          v.z = f = lora::chirp_fstep(f, cc);
+          v.w = f = lora::chirp_fstep(f, cc);
+        };
+        int k = 0;
+        for (; k + 2 <= a.step / 4; k += 2) {
+          float4 va, vb;
+          quad(va);
+          bc[k] = va;
+          quad(vb);
+          bc[k + 1] = vb;
+        }
+        if (k < a.step / 4) {
+          float4 va;
+          quad(va);
+          bc[k] = va;
         }
       }
       return;
@@ -790,55 +868,116 @@ __global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int 
       }
     }
   };
-  // window t's phases in place (lane 0 only)
+  // window t's phase additions (lane 0 only): the block starts into pst[t % 4]
   auto chain = [&](int t, float& phase) {
     const int64_t s0 = (int64_t)t * W;
-    const int n = (int)min((int64_t)W, total - s0);
-    float* b = buf[t % 3];
-    const int len = a.step <= W ? a.step : n;  // samples until the next chirp boundary
-    for (int c0 = 0; c0 < n; c0 += len) {
-      float* bc = b + c0;
-      if ((len & 15) == 0) {
-        float4 x[4], y[4];
+    const int n = wlen(t);
+    const float* b = buf[t % 4];
+    float* ps = pst[t % 4];
+    if (a.step % kMfBlk == 0) {
+      // chirp ends fall on block ends; two blocks in flight, each block's frequencies
+      // requested a block ahead (the loads past the window read its pad: unused); the
+      // scheduling barriers keep the requests where they are
+      float4 xa[kMfBlk / 4], xb[kMfBlk / 4];
+      auto ld = [&](float4* x, int i) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x[q] = reinterpret_cast<const float4*>(bc)[q];
-        for (int i = 0; i < len; i += 16) {
-          if (i + 16 < len) {
+        for (int q = 0; q < kMfBlk / 4; ++q) x[q] = reinterpret_cast<const float4*>(b + i)[q];
+      };
+      int left = a.step - (int)(s0 % a.step);  // samples to the next chirp end (one division per window)
+      auto run = [&](const float4* x, int i) {
+        ps[i / kMfBlk] = phase;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) y[q] = reinterpret_cast<const float4*>(bc + i + 16)[q];
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            phase += x[q].x;
-            x[q].x = phase;
-            phase += x[q].y;
-            x[q].y = phase;
-            phase += x[q].z;
-            x[q].z = phase;
-            phase += x[q].w;
-            x[q].w = phase;
-            reinterpret_cast<float4*>(bc + i)[q] = x[q];
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x[q] = y[q];
+        for (int q = 0; q < kMfBlk / 4; ++q) {
+          phase = phase + x[q].x;
+          phase = phase + x[q].y;
+          phase = phase + x[q].z;
+          phase = phase + x[q].w;
         }
-      } else {
-        for (int i = 0; i < len; ++i) {
-          phase += bc[i];
-          bc[i] = phase;
+        left -= kMfBlk;
+        if (left == 0) {
+          phase = mf_wrap(phase);
+          left = a.step;
+        }
+      };
+      ld(xa, 0);
+      ld(xb, kMfBlk);
+      int i = 0;
+      for (; i + 2 * kMfBlk <= n; i += 2 * kMfBlk) {
+        run(xa, i);
+        __builtin_amdgcn_sched_barrier(0);
+        ld(xa, i + 2 * kMfBlk);
+        __builtin_amdgcn_sched_barrier(0);
+        run(xb, i + kMfBlk);
+        __builtin_amdgcn_sched_barrier(0);
+        ld(xb, i + 3 * kMfBlk);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (i < n) run(xa, i);  // (n an odd number of blocks)
+    } else {
+      int left = a.step - (int)(s0 % a.step);
+      for (int i = 0; i < n; ++i) {
+        if (i % kMfBlk == 0) ps[i / kMfBlk] = phase;
+        phase += b[i];
+        if (--left == 0) {
+          phase = mf_wrap(phase);
+          left = a.step;
         }
       }
-      // ChirpGenerator.hpp:130 at each chirp's end
-      if ((s0 + c0 + len) % a.step == 0) phase = (float)((double)phase - floor((double)phase / (2 * M_PI)) * 2 * M_PI);
     }
   };
-  // window t's samples (ChirpGenerator.hpp:122: polar(ampl, phase))
+  // window t's phases, block by block from the recorded starts, in place of the frequencies
+  auto recompute = [&](int t) {
+    if (wk < 0 || wk >= nwk) return;
+    const int64_t s0 = (int64_t)t * W;
+    const int n = wlen(t);
+    float* b = buf[t % 4];
+    const float* ps = pst[t % 4];
+    const bool aligned = a.step % kMfBlk == 0;  // chirp ends only at block ends
+    for (int blk = wk; blk * kMfBlk < n; blk += nwk) {
+      float phase = ps[blk];
+      const int i0 = blk * kMfBlk, i1 = min(n, i0 + kMfBlk);
+      if (aligned) {
+        // a whole block: its frequencies in, 32 additions in registers, its phases out
+        float4 x[kMfBlk / 4];
+#pragma unroll
+        for (int q = 0; q < kMfBlk / 4; ++q) x[q] = reinterpret_cast<const float4*>(b + i0)[q];
+#pragma unroll
+        for (int q = 0; q < kMfBlk / 4; ++q) {
+          x[q].x = phase = phase + x[q].x;
+          x[q].y = phase = phase + x[q].y;
+          x[q].z = phase = phase + x[q].z;
+          x[q].w = phase = phase + x[q].w;
+        }
+#pragma unroll
+        for (int q = 0; q < kMfBlk / 4; ++q) reinterpret_cast<float4*>(b + i0)[q] = x[q];
+      } else {
+        int left = a.step - (int)((s0 + i0) % a.step);
+        for (int i = i0; i < i1; ++i) {
+          phase = phase + b[i];
+          b[i] = phase;
+          if (--left == 0) {
+            phase = mf_wrap(phase);
+            left = a.step;
+          }
+        }
+      }
+    }
+  };
+  // window t's samples (ChirpGenerator.hpp:122: polar(ampl, phase)), coalesced
   auto emit = [&](int t) {
     if (wk < 0 || wk >= nwk) return;
     const int64_t s0 = (int64_t)t * W;
-    const int n = (int)min((int64_t)W, total - s0);
-    const float* b = buf[t % 3];
-    for (int i = wk; i < n; i += nwk) {
+    const int n = wlen(t);
+    const float* b = buf[t % 4];
+    // two samples per lane at a time: two independent double-precision chains in flight
+    int i = wk;
+    for (; i + nwk < n; i += 2 * nwk) {
+      float sn[2], cs[2];
+      mod_sincosf2(b[i], b[i + nwk], sn, cs);
+      out[s0 + i] = cf{a.ampl * cs[0], a.ampl * sn[0]};
+      out[s0 + i + nwk] = cf{a.ampl * cs[1], a.ampl * sn[1]};
+    }
+    if (i < n) {
       float sn, cs;
       mod_sincosf(b[i], &sn, &cs);
       out[s0 + i] = cf{a.ampl * cs, a.ampl * sn};
@@ -847,17 +986,67 @@ __global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int 
   float phase = 0.0f;
   build(0);
   __syncthreads();
-  for (int t = 0; t < nwin + 2; ++t) {
+#ifdef LORA_MF_PROF
+  // diagnostics (results invalid): per iteration, shader cycles of the chain (lane 0) and of
+  // the fill / build / recompute / emit stages and the barrier (the first and the last
+  // worker lane), written over the frame's first samples at the end
+  __shared__ uint32_t prof[64][8];
+#endif
+  for (int t = 0; t < nwin + 3; ++t) {
+#ifdef LORA_MF_PROF
+    const uint64_t p0 = __builtin_amdgcn_s_memtime();
+    uint64_t p1 = p0, p2 = p0, p3 = p0, p4 = p0;
+#endif
     if (wk < 0) {
       if (tid == 0 && t >= 1 && t - 1 < nwin) chain(t - 1, phase);
+#ifdef LORA_MF_PROF
+      p1 = __builtin_amdgcn_s_memtime();
+#endif
     } else {
       fill(t);
+#ifdef LORA_MF_PROF
+      p1 = __builtin_amdgcn_s_memtime();
+#endif
       build(t + 1);
-      if (t >= 2) emit(t - 2);
+#ifdef LORA_MF_PROF
+      p2 = __builtin_amdgcn_s_memtime();
+#endif
+      if (t >= 2 && t - 2 < nwin) recompute(t - 2);
+#ifdef LORA_MF_PROF
+      p3 = __builtin_amdgcn_s_memtime();
+#endif
+      if (t >= 3) emit(t - 3);
+#ifdef LORA_MF_PROF
+      p4 = __builtin_amdgcn_s_memtime();
+#endif
     }
     __syncthreads();
+#ifdef LORA_MF_PROF
+    const uint64_t p5 = __builtin_amdgcn_s_memtime();
+    if (t < 64) {
+      if (tid == 0) {
+        prof[t][0] = (uint32_t)(p1 - p0);
+        prof[t][7] = (uint32_t)(p5 - p0);
+      }
+      if (wk == 0) {
+        prof[t][1] = (uint32_t)(p1 - p0);
+        prof[t][2] = (uint32_t)(p2 - p1);
+        prof[t][3] = (uint32_t)(p3 - p2);
+        prof[t][4] = (uint32_t)(p4 - p3);
+      }
+      if (wk == kMfWorkers - 1) {
+        prof[t][5] = (uint32_t)(p2 - p1);  // the last lane: a builder when there are runs
+        prof[t][6] = (uint32_t)(p4 - p0);
+      }
+    }
+#endif
   }
+#ifdef LORA_MF_PROF
+  __syncthreads();
+  for (int i = tid; i < 64 * 8; i += kMfThreads) reinterpret_cast<uint32_t*>(out)[i] = prof[i / 8][i % 8];
+#endif
 }
+
 }  // namespace
 
 // ===================================================================================
@@ -1332,6 +1521,57 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   return rc < 0 ? rc : nsym;
 }
 
+namespace {
+// The run tables of k_mod_runs per (device, sf, osr, bandwidth), kept for the process's
+// lifetime: chirp values below max(N, 256) (symbols, sync nibbles, lora_encode's 8-bit
+// codewords); a larger value's chirp is derived in the frame kernel itself.  SF12 osr 1:
+// 4,096 x 92 runs x 16 B = 6 MB.
+struct ModRunTable {
+  int device, sf, osr;
+  float bw_scale;
+  int n, cap;
+  lora::ChirpSeg* seg;
+  int* cnt;
+};
+std::mutex g_mrt_mu;
+std::vector<ModRunTable> g_mrt;
+
+// fills a.seg / cnt / seg_n / seg_cap; false (g_last_error set) if the tables could not be made
+bool mod_run_table(ModArgs& a, int sf, hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error(LORA_EIO, "hipGetDevice"), false;
+  std::lock_guard<std::mutex> lk(g_mrt_mu);
+  for (const ModRunTable& t : g_mrt)
+    if (t.device == dev && t.sf == sf && t.osr == a.osr && t.bw_scale == a.bw_scale) {
+      a.seg = t.seg;
+      a.cnt = t.cnt;
+      a.seg_n = t.n;
+      a.seg_cap = t.cap;
+      return true;
+    }
+  ModRunTable t{dev, sf, a.osr, a.bw_scale, std::max(a.N, 256), lora::chirp_seg_cap(sf), nullptr, nullptr};
+  if (hipMalloc(&t.seg, sizeof(lora::ChirpSeg) * (size_t)t.n * t.cap) != hipSuccess ||
+      hipMalloc(&t.cnt, sizeof(int) * (size_t)t.n) != hipSuccess) {
+    if (t.seg) hipFree(t.seg);
+    return set_error(LORA_EIO, "hipMalloc"), false;
+  }
+  // (recorded with the frame kernel when the C++ drop-in dispatches on its AQL queue: the
+  // packets run in order; otherwise built and waited for here, once)
+  lora::launch(k_mod_runs, dim3((unsigned)((t.n + 63) / 64)), dim3(64), 0, st, a, t.n, t.cap, t.seg, t.cnt);
+  if (!lora::t_launch_record && hipStreamSynchronize(st) != hipSuccess) {
+    hipFree(t.seg);
+    hipFree(t.cnt);
+    return set_error(LORA_EIO, "k_mod_runs"), false;
+  }
+  g_mrt.push_back(t);
+  a.seg = t.seg;
+  a.cnt = t.cnt;
+  a.seg_n = t.n;
+  a.seg_cap = t.cap;
+  return true;
+}
+}  // namespace
+
 int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitude, uint8_t sync,
                        const uint16_t* symbols, int64_t frames, int64_t sym_count, float* iq,
                        int device, void* stream) {
@@ -1372,8 +1612,16 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
   // short ones 64 frames per wave (their chains are short: the lanes' issue count matters)
   a.fpw = step >= 1024 ? 1 : 64;
   while (a.fpw < 64 && (int64_t)a.fpw * 1024 < frames) a.fpw *= 2;
+  a.seg = nullptr;
+  a.cnt = nullptr;
+  a.seg_n = a.seg_cap = 0;
   if (frames <= kMfMaxFrames) {
-    // few frames: a workgroup per frame, windows of whole chirps or exact chirp fractions
+    // few frames: a workgroup per frame, windows of whole chirps or exact chirp fractions;
+    // long chirps from the configuration's run tables (built here on first use)
+    if (step >= kMfTabMin && !mod_run_table(a, (int)sf, st)) {
+      if (prev != device) hipSetDevice(prev);
+      return set_error(LORA_EIO, "modulator run tables: " + g_last_error);
+    }
     const int W = step <= kMfWin ? step * (kMfWin / step) : step / ((step + kMfWin - 1) / kMfWin);
     const int64_t nwin = (per_frame + W - 1) / W;
     lora::launch(k_mod_frame, dim3((unsigned)frames), dim3(kMfThreads), 0, st, a, W, (int)nwin);
@@ -1460,3 +1708,4 @@ int64_t lora_compensate_offsets_batch(unsigned sf, unsigned osr, const float* in
 }
 
 }  // extern "C"
+

@@ -64,14 +64,12 @@ LC_FN int lc_binade(float f) {
   return (e == 0 || e == 0xff) ? -1 : (int)(b >> 23);
 }
 
-// 2^(e+1) for the binade of |f| (f normal)
+// 2^(e+1) for the binade [2^e, 2^(e+1)) of |f| (f normal): built from the exponent bits
 LC_FN double lc_top(float f) {
-  const int e = (int)((lc_bits(f) >> 23) & 0xff) - 127;
-  double t = 1.0;
-  if (e + 1 >= 0)
-    for (int i = 0; i < e + 1; ++i) t *= 2.0;
-  else
-    for (int i = 0; i < -(e + 1); ++i) t *= 0.5;
+  const uint64_t e = (lc_bits(f) >> 23) & 0xff;  // biased: 2^(e - 127 + 1) = double exponent e - 127 + 1 + 1023
+  const uint64_t d = (e + 897u) << 52;
+  double t;
+  __builtin_memcpy(&t, &d, 8);
   return t;
 }
 
@@ -104,14 +102,16 @@ LC_FN int chirp_segments(float f_init, int n, const ChirpConst& c, ChirpSeg* seg
       const bool in_bin = f > 0.0f ? (vprev + fs < top) : (vprev + fs <= -top * 0.5);
       return in_bin && v <= (double)c.fMax;
     };
-    // candidate from the bounds, then corrected by the exact conditions (monotone in j)
+    // candidate from the bounds (one reciprocal: the estimate may be off by one either way),
+    // then corrected by the exact conditions (monotone in j)
     double lim = (double)(n - k);
+    const double inv = 1.0 / dd;
     if (f > 0.0f) {
-      const double a = (top - fs - fd) / dd + 1.0, b = ((double)c.fMax - fd) / dd;
+      const double a = (top - fs - fd) * inv + 1.0, b = ((double)c.fMax - fd) * inv;
       lim = a < lim ? a : lim;
       lim = b < lim ? b : lim;
     } else {
-      const double a = (-top * 0.5 - fs - fd) / dd + 1.0;
+      const double a = (-top * 0.5 - fs - fd) * inv + 1.0;
       lim = a < lim ? a : lim;
     }
     int64_t L = lim > 0.0 ? (int64_t)lim : 0;

@@ -915,13 +915,12 @@ constexpr size_t spec_dtl_offset() {
 // SF 6-8: instead of the table-phase-0 slice, the whole doubled dechirp table (KArgs::down,
 // 2N entries: 1-4 KB), so a window at any table phase - every frame with t_off != 0, i.e.
 // every captured frame - reads its table values from LDS too (four workgroups per CU still
-// fit); SF9 keeps the slice (its 8 KB table would cost the fourth workgroup).
-#ifndef LORA_DTAB
-#define LORA_DTAB 1
-#endif
+// fit); SF9 keeps the slice (its 8 KB table would cost the fourth workgroup).  Same-box A/B
+// against the slice (tools/r05_ab.py, three interleaved runs): SF7 symbol pass 0.2187 ->
+// 0.2146 ms noiseless, 0.2467 -> 0.2352 at 0 dB, 0.2523 -> 0.2390 at -10 dB.
 template <int SF>
 constexpr bool spec_dtab() {
-  return LORA_DTAB && Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2 &&
+  return Geo<SF>::WAVE_LOCAL && Geo<SF>::NPASS == 2 &&
          4 * (spec_dtl_offset<SF>() + 2 * sizeof(cf) * Geo<SF>::N) <= 160 * 1024;
 }
 template <int SF>

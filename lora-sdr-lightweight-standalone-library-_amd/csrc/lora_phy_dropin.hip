@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <ctime>
 #include <cstring>
 #include <mutex>
 
@@ -71,6 +72,15 @@ uint16_t sx1272_data_checksum(const uint8_t* data, int length) {
 }
 
 size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+// lora_phy_dropin_last_timing: the last AQL demodulation's and modulation's phases (us)
+double g_timing[8] = {};
+
+double now_us() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return 1e6 * (double)t.tv_sec + 1e-3 * (double)t.tv_nsec;
+}
 
 // One frame's IQ, symbols and per-frame outputs, then the batch workspace: the same
 // layout in the device allocation and in the pinned host staging.
@@ -236,8 +246,10 @@ int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* 
                   FrameOut& out, int64_t nsym, const DevLayout& d) {
   unsigned char* dev = static_cast<unsigned char*>(g.dev);
   unsigned char* host = static_cast<unsigned char*>(g.host);
+  const double t0 = now_us();
   if (count > 0 && samples != reinterpret_cast<const std::complex<float>*>(host + d.iq))
     std::memcpy(host + d.iq, samples, count * sizeof(std::complex<float>));
+  const double t1 = now_us();
   lora_demod_outputs o{};
   o.symbols = reinterpret_cast<uint16_t*>(host + d.syms);
   o.sym_stride = std::max<int64_t>(nsym, 1);
@@ -252,22 +264,31 @@ int run_frame_aql(lora_phy::detail::device_state& g, const std::complex<float>* 
   if (g.shared_aql || g.shared_plan) lk.lock();
   lora::LaunchRecord rec;
   lora::t_launch_record = &rec;
+  // (the kernels read the frame in the staging across the host link: copying it into device
+  // memory first - one more packet - cost more than it saved, 42.3 vs 38.8 us per SF7 frame,
+  // and non-coherent staging changed nothing; tools/r05_dropin_ab.sh)
   const int64_t rc = lora_demod_batch(g.plan, reinterpret_cast<const float*>(host + d.iq), 1, (int64_t)count,
                                       (int64_t)count, &o, dev + d.ws, d.total - d.ws, g.stream);
   lora::t_launch_record = nullptr;
   if (rc < 0) return 0;
   if (rec.bad) return -1;
+  const double t2 = now_us();
   if (rec.n > 0) {
     const int e = lora::aql_run(static_cast<lora::AqlQueue*>(g.aql), rec);
     if (e != 0) return e;
   }
   lk.unlock();
+  const double t3 = now_us();
   out.nsym = nsym;
   out.sync = host[d.sync];
   std::memcpy(&out.cfo, host + d.cfo, 4);
   std::memcpy(&out.toff, host + d.toff, 4);
   std::memcpy(&out.max_amp, host + d.maxa, 4);
   out.syms = reinterpret_cast<const uint16_t*>(host + d.syms);
+  g_timing[0] = t1 - t0;
+  g_timing[1] = t2 - t1;
+  g_timing[2] = t3 - t2;
+  g_timing[3] = now_us() - t3;  // (the caller's copy of the symbols follows)
   return 1;
 }
 
@@ -504,14 +525,22 @@ size_t lora_modulate(const uint16_t* symbols, size_t symbol_count, std::complex<
     std::lock_guard<std::mutex> lk(R.mu);
     uint16_t* hs = static_cast<uint16_t*>(R.mod_host);
     float* hiq = reinterpret_cast<float*>(static_cast<unsigned char*>(R.mod_host) + align256(kModSyms * 2));
+    const double t0 = now_us();
     if (symbol_count > 0) std::memcpy(hs, symbols, symbol_count * 2);
+    const double t1 = now_us();
     lora::LaunchRecord rec;
     lora::t_launch_record = &rec;
     const int64_t r = lora_mod_batch(sf, osr, static_cast<unsigned>(bw), amplitude, sync, hs, 1,
                                      (int64_t)symbol_count, hiq, R.device, nullptr);
     lora::t_launch_record = nullptr;
+    const double t2 = now_us();
     if (r >= 0 && !rec.bad && rec.n > 0 && lora::aql_run(R.aql, rec) == 0) {
+      const double t3 = now_us();
       std::memcpy(out_samples, hiq, per * 8);
+      g_timing[4] = t1 - t0;
+      g_timing[5] = t2 - t1;
+      g_timing[6] = t3 - t2;
+      g_timing[7] = now_us() - t3;
       return per;
     }
     // otherwise (a launch the queue does not take) the HIP path below
@@ -852,3 +881,8 @@ void ensure_runtime() {
 // LORA_MI355X_DROPIN_LAZY and no drop-in call made yet, 2: no HIP device, 3-6: plans / buffers, a negative aql_create
 // code, 7-8 / -13x: the warm-up)
 extern "C" int lora_phy_dropin_status(void) { return rt().status; }
+
+extern "C" int lora_phy_dropin_last_timing(double* out) {
+  for (int i = 0; i < 8; ++i) out[i] = g_timing[i];
+  return 8;
+}

@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
     lora_phy::lora_demod_workspace ws{};
     lora_phy::lora_demod_init(&ws, sf, lora_phy::window_type::window_none, scratch.data(), scratch.size());
     const int n = sf >= 12 ? std::max(packets / 10, 20) : packets;
-    std::vector<double> tm, td, tdm, tall;
+    std::vector<double> tm, td, tdm, tall, phs[8];
     std::string mod_tl = "null", dem_tl = "null";
     bool ok = true;
     for (int p = 0; p < warm + n; ++p) {
@@ -79,6 +79,9 @@ int main(int argc, char** argv) {
       const double t4 = now_us();
       if (p == warm + n - 1) dem_tl = timeline();
       if (p >= warm) {
+        double b[8];
+        lora_phy_dropin_last_timing(b);
+        for (int k = 0; k < 8; ++k) phs[k].push_back(b[k]);
         tm.push_back(t1 - t0);
         td.push_back(t3 - t2);
         tdm.push_back(t4 - t3);
@@ -89,9 +92,13 @@ int main(int argc, char** argv) {
     lora_phy::lora_demod_free(&ws);
     std::printf(
         "{\"sf\": %u, \"packets\": %d, \"symbols_ok\": %s, \"modulate_us\": %.2f, \"dechirp_us\": %.2f, "
-        "\"demodulate_us\": %.2f, \"packet_us\": %.2f, \"pps\": %.1f, \"modulate_aql\": %s, \"demodulate_aql\": %s}\n",
+        "\"demodulate_us\": %.2f, \"packet_us\": %.2f, \"pps\": %.1f, "
+        "\"demodulate_phases_us\": {\"copy_in\": %.2f, \"host_logic\": %.2f, \"aql_run\": %.2f, \"copy_out\": %.2f}, "
+        "\"modulate_phases_us\": {\"copy_in\": %.2f, \"host_logic\": %.2f, \"aql_run\": %.2f, \"copy_out\": %.2f}, "
+        "\"modulate_aql\": %s, \"demodulate_aql\": %s}\n",
         sf, n, ok ? "true" : "false", median(tm), median(td), median(tdm), median(tall), 1e6 / median(tall),
-        mod_tl.c_str(), dem_tl.c_str());
+        median(phs[0]), median(phs[1]), median(phs[2]), median(phs[3]), median(phs[4]), median(phs[5]), median(phs[6]),
+        median(phs[7]), mod_tl.c_str(), dem_tl.c_str());
     std::fflush(stdout);
   }
   return 0;

@@ -21,9 +21,11 @@ LIB = os.path.join(ROOT, "lora-sdr-lightweight-standalone-library-_amd", "lora_p
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
-# the kernels lora_demod_batch launches through lora::launch (recorded for the AQL queue)
-FAMILIES = ("k_spec_demod", "k_est_split", "k_est_fast", "k_demod_fast", "k_frame_max_wave", "k_frame_max",
-            "k_estimate")
+# the kernels lora_demod_batch and lora_mod_batch launch through lora::launch (recorded for the
+# AQL queue)
+FAMILIES = ("k_spec_demod", "k_est_split", "k_cert_split", "k_spec_fix", "k_est_fast", "k_demod_fast",
+            "k_frame_max_wave", "k_frame_max", "k_estimate", "k_mod_phase", "k_mod_samples", "k_mod_frame",
+            "k_mod_runs")
 V5 = {"hidden_block_count_x": 0, "hidden_block_count_y": 4, "hidden_block_count_z": 8,
       "hidden_group_size_x": 12, "hidden_group_size_y": 14, "hidden_group_size_z": 16,
       "hidden_remainder_x": 18, "hidden_remainder_y": 20, "hidden_remainder_z": 22,

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """One bench workload alone, for a profiler: the pipeline over `frames` frames of 2 + 64
 symbols (bench.py's make_input: GPU modulation, optional AWGN at `snr` dB), `steps`
-times.  usage: prof_workload.py <sf> [snr_db|none] [frames] [steps] [data_symbols] [osr]"""
+times.  usage: prof_workload.py <sf> [snr_db|none] [frames] [steps] [data_symbols] [osr] [mode]
+(mode: legacy (default), api or raw - bench.py's receiver lines)"""
 import os
 import sys
 
@@ -19,9 +20,10 @@ frames = int(sys.argv[3]) if len(sys.argv) > 3 else 15625
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 data_syms = int(sys.argv[5]) if len(sys.argv) > 5 else 64
 osr = int(sys.argv[6]) if len(sys.argv) > 6 else 1
+mode = sys.argv[7] if len(sys.argv) > 7 else "legacy"
 dev = torch.device("cuda", 0)
 _, iq = bench.make_input(sf, frames, data_syms, 20251015, dev, snr, osr=osr)
-plan = amd.DemodPlan(sf, osr, 125000, "none", dechirp=True, mode="legacy", device=dev)
+plan = amd.DemodPlan(sf, osr, 125000, "none", dechirp=True, mode=mode, device=dev)
 out = None
 for _ in range(steps):
     out = plan.run(iq, out)

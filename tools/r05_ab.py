@@ -5,7 +5,7 @@ usage: python tools/r05_ab.py [--reps 3] [--steps 100] [--work sf7,awgn0,awgn10,
   (tools/build_variant.sh).  Each (rep, variant) runs in its own process, interleaved;
   prints one line per run: variant, then per workload ms_per_step and the symbol-pass ms.
 Workloads: sf7 (headline), awgn0 / awgn10 (SF7 at 0 / -10 dB), sf12, sf12n (SF12 -10 dB),
-osr2, hann.
+osr2, hann; mod7 / mod12 (the modulator on 15,625 frames: ms per call, write-peak fraction).
 """
 import argparse
 import json
@@ -36,6 +36,11 @@ def child(works, steps):
     dev = torch.device("cuda", 0)
     out = {}
     for w in works:
+        if w.startswith("mod"):  # modulator: bench.run_modulator, ms per call
+            sf = int(w[3:])
+            r = bench.run_modulator(sf, 15625, 64, dev, with_cpu=False)
+            out[w] = [round(r["ms_per_call"], 4), round(r["roofline_frac"], 4)]
+            continue
         kw = dict(WORK[w])
         sf, frames = kw.pop("sf"), kw.pop("frames")
         st = steps if sf < 12 else max(steps // 4, 4)
