@@ -18,8 +18,14 @@ for k, v in d["extra"].items():
     if "roofline" in v:
         out["frac"] = round(v["roofline"]["frac"], 4)
         out["pipeline_frac"] = round(v["roofline"]["pipeline"]["pipeline_frac"], 4)
+    par = v.get("parity") or (v.get("cpu_baseline") or {}).get("parity_ok")
+    if isinstance(par, dict):
+        out["parity_ok"] = par.get("parity_ok", par.get("symbol_agreement_with_exact"))
+    elif par is not None:
+        out["parity_ok"] = par
     if "three_launch" in v:
         out["three_launch_ms"] = round(v["three_launch"]["ms_per_step"], 4)
     print(k, out)
 c = d.get("cpu_baseline") or {}
-print("cpu", c.get("value"), c.get("cores"), c.get("kind"))
+print("cpu", c.get("value"), c.get("cores"), c.get("kind"), "reference_parity", (c.get("reference_parity") or {}).get("parity_ok"))
+print("headline parity", d["config"].get("parity"))
