@@ -22,7 +22,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAGS = {"kt7": "SF7 headline (15,625 frames x 66 symbols, noiseless)",
         "kt7n10": "SF7 at -10 dB AWGN (same shape)",
         "kt12": "SF12 (15,625 frames x 66 symbols, noiseless)",
-        "kt7o2": "SF7 osr 2 (15,625 frames x 66 symbols, noiseless)"}
+        "kt7o2": "SF7 osr 2 (15,625 frames x 66 symbols, noiseless)",
+        "kt7n0": "SF7 at 0 dB AWGN (same shape)",
+        "kt7o4": "SF7 osr 4 (15,625 frames x 66 symbols, noiseless)",
+        "kt7api": "SF7 API mode (phy::demodulate, same shape)",
+        "kt7raw": "SF7 RAW mode (detector per symbol, same shape)"}
+ROUND = os.environ.get("PROF_ROUND", "4")
 
 
 def short(name):
@@ -45,7 +50,7 @@ def main():
     res = {}
     for r in kernel_resources.kernels(os.path.join(ROOT, kernel_resources.LIB)):
         res.setdefault(short(r.get("demangled", r["name"])), r)
-    out = ["# Round-4 kernel statistics (rocprofv3 --kernel-trace --stats)", "",
+    out = [f"# Round-{ROUND} kernel statistics (rocprofv3 --kernel-trace --stats)", "",
            "Each workload alone (`tools/prof_workload.py`, eager `plan.run` per step).  Resources: code-object "
            "metadata of the built `liblora_mi355x.so` (`tools/kernel_resources.py`); `LDS B (launch)` is the "
            "trace's allocation for the launch (static + dynamic).  The tracer serialises dispatches; bench.py's "
@@ -111,7 +116,7 @@ def main():
             cnt[k][n] += 1
     if per:
         out += ["## SQ counters per launch (summed over XCDs / SEs, averaged over launches)", "",
-                "SF7 workloads: 15,625 frames; SF12: 4,000 frames (tools/r04_prof.sh).", ""]
+                f"SF7 workloads: 15,625 frames; SF12: 4,000 frames (tools/r0{ROUND}_prof.sh).", ""]
         for k in sorted(per):
             if not k.startswith(("k_spec_demod", "k_est", "k_cert")):
                 continue
