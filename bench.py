@@ -4,9 +4,10 @@ One step = one lora_demod_batch over this rank's batch of frames already residen
 HBM: LEGACY lora_demodulate semantics with the fused caller-side dechirp
 (e2e_chain_test.cpp:85-101): normalisation, 2-symbol CFO/timing estimate, per-symbol
 CFO rotation, FFT, argmax, sync word.  Inputs are generated on the device by the
-bit-exact GPU modulator (lora_mod_batch), random symbols from a fixed seed.  The step's
-launches are captured once into a HIP graph and replayed per step (`--launch eager`:
-plan.run per step, ~1.5 % slower at SF7 from host launch overhead).
+bit-exact GPU modulator (lora_mod_batch), random symbols from a fixed seed.  Each step is
+one plan.run (the pipeline's four kernels enqueued on the stream; `--launch graph` replays
+them as a captured HIP graph instead, whose per-replay cost made it 2 % slower at SF7 in
+round 5's same-box A/B, tools/r05_launch_ab.sh).
 
 Headline workload (BASELINE.json configs[1]): SF7 BW125 osr 1, 1,000,000 data symbols
 = 15,625 frames x (2 sync + 64 data) per GPU.  The SF12 configuration (configs[2]) and
@@ -178,7 +179,7 @@ def make_input(sf, frames, data_syms, seed, device, snr_db=None, sync=None, osr=
     return syms, iq
 
 
-LAUNCH = "graph"  # --launch: "graph" (HIP graph replay of the step, default) or "eager" (plan.run)
+LAUNCH = "eager"  # --launch: "eager" (plan.run per step, default) or "graph" (HIP graph replay of the step)
 
 
 def stage_times(plan, iq, out, steps, device):
@@ -695,9 +696,11 @@ def roofline(r, probe=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--launch", choices=["eager", "graph"], default="graph",
-                    help="step launch: one HIP-graph replay of the step's launches (default; the same "
-                         "kernels on the same buffers, captured once), or plan.run per step")
+    ap.add_argument("--launch", choices=["eager", "graph"], default="eager",
+                    help="step launch: plan.run per step (default: the step's four kernels enqueued on the "
+                         "stream, about 1.5-2 us between dependent kernels), or one HIP-graph replay of the "
+                         "step's launches (the same kernels on the same buffers, captured once; each replay "
+                         "adds about 9.5 us before the next step - round 5: 2 % slower, tools/r05_launch_ab.sh)")
     # 100 timed steps (33 ms at SF7): with 20 (6 ms) a single host or clock hiccup moved the
     # per-step time by several percent between runs of the same build
     ap.add_argument("--steps", type=int, default=100)

@@ -69,6 +69,59 @@ def kernels(path):
     return rows
 
 
+# ---- the dynamic LDS each launch requests (lora_demod_fast.hip's launch_* functions),
+# restated from its constexpr formulas: lds_row<SF>() = N + W3 + sum(LdsMap<SF>::W) + PAD,
+# spec_lds_bytes<SF>(), the estimate / certification / fix kernels' row sets
+LDS_MAP = {6: (0, (1, 2), 1), 7: (1, (1, 2, 4), 0), 8: (0, (1, 2, 4, 8), 1), 9: (0, (0, 1, 4, 8, 14), 0),
+           10: (0, (0, 0, 1, 2, 4, 8), 0), 11: (0, (0, 0, 2, 8, 10, 20, 43), 0),
+           12: (0, (0, 0, 0, 0, 1, 2, 4, 8), 0)}
+
+
+def geo(sf):
+    N = 1 << sf
+    T = N // 16
+    R1 = 8 if sf & 1 else 16
+    X = N // R1
+    RA = 16 if X >= 16 else X
+    npass = 1 + (X > 1) + (X > 16)
+    w3, w, pad = LDS_MAP[sf]
+    return {"N": N, "T": T, "SPW": 256 // T, "MA_A": R1, "RA": RA, "NPASS": npass, "WL": T <= 64,
+            "rowc": N + w3 + sum(w) + pad}
+
+
+def dynamic_lds(demangled):
+    """Dynamic LDS bytes the host requests for a launch of this kernel (SF >= 6), or None."""
+    # the modulator, frame-max and compensation kernels use static LDS only
+    if re.match(r"void (k_mod_\w+|k_frame_max\w*|k_compensate)\b", demangled):
+        return 0
+    m = re.match(r"void (k_\w+)<(\d+)(?:, (\w+))?(?:, (\w+))?(?:, (\w+))?>", demangled)
+    if not m or int(m.group(2)) < 6 or int(m.group(2)) > 12:
+        return None
+    k, sf = m.group(1), int(m.group(2))
+    g = geo(sf)
+    twl = (15 if g["RA"] == 16 else 3) * g["MA_A"]
+    if k == "k_spec_demod":
+        dtl_off = ((g["SPW"] * g["rowc"] + twl) * 8 + 15) & ~15
+        pf2 = g["WL"] and g["NPASS"] == 2
+        if not pf2:
+            return 8 * (g["SPW"] * g["rowc"] + twl)
+        dtab = 4 * (dtl_off + 16 * g["N"]) <= 160 * 1024
+        return dtl_off + (16 * g["N"] if dtab else 128 * g["T"])
+    if k in ("k_est_split", "k_cert_split"):
+        return 8 * 2 * (64 // (2 * g["T"])) * g["rowc"]
+    if k == "k_spec_fix":
+        return 8 * g["SPW"] * g["rowc"]
+    if k == "k_est_fast":
+        mode = int(m.group(3))
+        block = 256 if g["T"] >= 64 else 64
+        pair = sf >= 7 and g["WL"] and g["NPASS"] == 2 and mode <= 1
+        return 8 * (block // g["T"]) * g["rowc"] * (2 if pair else 1)
+    if k == "k_demod_fast":
+        spec = m.group(5) == "true"
+        return 8 * (g["SPW"] * g["rowc"] + (twl if spec else 0))
+    return None
+
+
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     lib = args[0] if args and args[0].endswith(".so") else LIB

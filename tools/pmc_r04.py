@@ -5,7 +5,7 @@ from MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of a wide coalesced r
 doubled).  Writes <out>.md and profiles/pmc_summary.json (read by bench.py for
 roofline.traffic): per workload the dominant kernel's HBM bytes per launch and the step's.
 
-usage: pmc_r04.py <gpurun_out/prof4> <profiles/r04/pmc_traffic.md>"""
+usage: [PROF_ROUND=5] pmc_r04.py <gpurun_out/prof4> <profiles/r04/pmc_traffic.md>"""
 import collections
 import csv
 import glob
@@ -35,24 +35,32 @@ def per_kernel(d, counter):
 
 # algorithmic bytes per launch of the dominant kernel: data symbols x (8N + 2)
 # workload: (tag of the pmc_* dirs, sf, frames, data symbols, osr)
-WL = {"sf7": ("7", 7, 15625, 64, 1), "sf12": ("12", 12, 4000, 64, 1), "osr2_sf7": ("7o2", 7, 15625, 64, 2)}
-summary, lines = {}, ["# HBM traffic per launch, rocprofv3 FETCH_SIZE / WRITE_SIZE (r04)", "",
+WL = {"sf7": ("7", 7, 15625, 64, 1), "sf12": ("12", 12, 4000, 64, 1), "osr2_sf7": ("7o2", 7, 15625, 64, 2),
+      # round 5 (tools/r05_prof.sh): osr 4, and bench.py's API / RAW receiver lines, whose
+      # symbol pass is k_demod_fast (RAW: every symbol an output)
+      "osr4_sf7": ("7o4", 7, 15625, 64, 4), "api_sf7": ("7api", 7, 15625, 64, 1), "raw_sf7": ("7raw", 7, 15625, 64, 1)}
+ROUND = os.environ.get("PROF_ROUND", "4")
+summary, lines = {}, [f"# HBM traffic per launch, rocprofv3 FETCH_SIZE / WRITE_SIZE (r0{ROUND})", "",
                       "FETCH_SIZE / WRITE_SIZE in KB as reported; `read B (x2)` applies the gfx950 correction "
                       "(MI355X_MICROARCH.md: FETCH_SIZE = half the bytes of a coalesced read).  Workloads: "
                       "`tools/prof_workload.py` (noiseless 2 + 64-symbol frames; SF7 15,625 frames, SF12 4,000, SF7 osr 2 15,625).", "",
                       "| workload | kernel | FETCH_SIZE KB | read B (x2) | WRITE_SIZE KB | HBM B/launch | algorithmic B | ratio |",
                       "|---|---|---:|---:|---:|---:|---:|---:|"]
 for wl, (tag, sf, frames, S, osr) in WL.items():
+    if not os.path.isdir(os.path.join(src, f"pmc_fetch{tag}")):
+        continue
     fe = per_kernel(os.path.join(src, f"pmc_fetch{tag}"), "FETCH_SIZE")
     wr = per_kernel(os.path.join(src, f"pmc_write{tag}"), "WRITE_SIZE")
     N = 1 << sf
     # the symbol pass reads every symbol's window (the sync symbols' too) and writes one
-    # u16 index per data symbol
-    algo = {"k_spec_demod": frames * ((S + 2) * 8 * N * osr + 2 * S)}
+    # u16 index per data symbol; the three-launch demod (API / RAW lines) reads and writes
+    # its output symbols only (RAW: all S + 2)
+    out_syms = S + 2 if wl.startswith("raw") else S
+    algo = {"k_spec_demod": frames * ((S + 2) * 8 * N * osr + 2 * S), "k_demod_fast": frames * out_syms * (8 * N + 2)}
     step = 0.0
     d = {"step_kernels": {}}
     for k in sorted(fe):
-        if not k.startswith(("k_spec", "k_est")):
+        if not k.startswith(("k_spec", "k_est", "k_cert", "k_demod_fast", "k_frame_max")):
             continue
         hbm = fe[k] * 1024 * 2 + wr.get(k, 0.0) * 1024
         step += hbm
@@ -60,7 +68,7 @@ for wl, (tag, sf, frames, S, osr) in WL.items():
         a = algo.get(k.split("<")[0])
         lines.append(f"| {wl} | `{k}` | {fe[k]:.0f} | {fe[k] * 2048:.4g} | {wr.get(k, 0.0):.0f} | {hbm:.4g} | "
                      f"{a if a else '-'} | {hbm / a if a else float('nan'):.4f} |")
-        if k.startswith("k_spec_demod"):
+        if k.startswith("k_spec_demod") or (k.startswith("k_demod_fast") and "kernel" not in d):
             d.update({"kernel": k, "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": a,
                       "traffic_over_algorithmic": hbm / a})
     step_algo = frames * ((S + 2) * (8 * N * osr + 2) + 9)

@@ -52,8 +52,9 @@ def main():
         res.setdefault(short(r.get("demangled", r["name"])), r)
     out = [f"# Round-{ROUND} kernel statistics (rocprofv3 --kernel-trace --stats)", "",
            "Each workload alone (`tools/prof_workload.py`, eager `plan.run` per step).  Resources: code-object "
-           "metadata of the built `liblora_mi355x.so` (`tools/kernel_resources.py`); `LDS B (launch)` is the "
-           "trace's allocation for the launch (static + dynamic).  The tracer serialises dispatches; bench.py's "
+           "metadata of the built `liblora_mi355x.so` (`tools/kernel_resources.py`); LDS = the metadata's static "
+           "bytes + the dynamic bytes the launch requests (`kernel_resources.dynamic_lds`, the launch formulas of "
+           "lora_demod_fast.hip restated; the trace's LDS_Block_Size shows only the static part).  The tracer serialises dispatches; bench.py's "
            "HIP-event stage times are measured without it.", ""]
     for tag, what in TAGS.items():
         rows = trace(os.path.join(src, tag))
@@ -65,7 +66,7 @@ def main():
             a["n"] += 1
             a["ns"].append(e - b)
         out += [f"## {tag}: {what}", "",
-                "| kernel | workgroups | launches | avg us | min us | max us | LDS B (launch) | VGPR | AGPR | "
+                "| kernel | workgroups | launches | avg us | min us | max us | LDS B (static + dynamic) | VGPR | AGPR | "
                 "scratch B/lane | VGPR spills |",
                 "|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
         for (k, wg), a in sorted(agg.items(), key=lambda kv: -sum(kv[1]["ns"])):
@@ -73,8 +74,11 @@ def main():
                 continue
             r = res.get(k, {})
             ns = a["ns"]
+            st = r.get("group_segment_fixed_size")
+            dy = kernel_resources.dynamic_lds("void " + k)
+            lds = f"{st} + {dy}" if st is not None and dy is not None else (f"{st} + ?" if st is not None else "?")
             out.append(f"| `{k}` | {wg} | {a['n']} | {sum(ns) / len(ns) / 1e3:.2f} | {min(ns) / 1e3:.2f} | "
-                       f"{max(ns) / 1e3:.2f} | {a['lds']} | {r.get('vgpr_count', '?')} | {r.get('agpr_count', '?')} | "
+                       f"{max(ns) / 1e3:.2f} | {lds} | {r.get('vgpr_count', '?')} | {r.get('agpr_count', '?')} | "
                        f"{r.get('private_segment_fixed_size', '?')} | {r.get('vgpr_spill_count', '?')} |")
         pipe = [r for r in rows if r[0].startswith(("k_est", "k_cert", "k_spec"))]
         gaps = sorted(pipe[i + 1][1] - pipe[i][2] for i in range(len(pipe) - 1))
