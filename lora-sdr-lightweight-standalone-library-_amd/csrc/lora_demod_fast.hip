@@ -1294,7 +1294,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
     struct Blk {
       int64_t f;
       int s, d, cg;
-      bool valid, mis;
+      bool valid, mis, nbr;
       float rate;
       int toff;
     };
@@ -1316,9 +1316,18 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
 #pragma unroll
       for (int q = 0; q < P; ++q)
         nx[q] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
-      if (B.mis)
-        nx[P] = __builtin_bit_cast(
-            v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, l < B.d ? vo : vo - T * 8, P * T * 8, 2 /* nt */));
+      B.nbr = false;
+      if (B.mis) {
+        // a late lane's 17th point is the next window's first: when that window is the next
+        // group's (the frame's next symbol, contiguous), taken from it by a lane permute
+        // where the block is consumed, so the line the two windows share is fetched once
+        int64_t bnext;
+        int cgn;
+        sym_base(B.s + 1, N, a.frame_len, B.toff, bnext, cgn);
+        B.nbr = gi < SPB - 1 && jl + 1 < per && bnext == base + N;
+        if (l < B.d && !B.nbr)
+          nx[P] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, P * T * 8, 2 /* nt */));
+      }
     };
     int64_t b = grp0 * BPG + wave;
     Blk nb{};
@@ -1355,6 +1364,10 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       // select (a misaligned window), dechirp, window max
       if (B.mis) {
         const bool late = l < d;
+        // the next group's first point (lane + T), before any lane shifts its points
+        const int src = ((int)__lane_id() + T) & 63;
+        const v2f n0 = {__shfl(ld[0].x, src, 64), __shfl(ld[0].y, src, 64)};
+        if (late && B.nbr) ld[P] = n0;
 #pragma unroll
         for (int q = 0; q < P; ++q) ld[q] = late ? ld[q + 1] : ld[q];
       }
