@@ -2160,19 +2160,29 @@ k_est_split(KArgs a, int64_t frames, int rowc) {
     for (int o = T; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
   };
-  // the pre-pass works on the unscaled samples (LoRaDemod.cpp:59-77 comes later: the
-  // frame maximum is only known after the symbol pass)
-  const int scaled = 0;
-  const float scale = 1.0f;
+  // LoRaDemod.cpp:59-77 normalises by the frame's maximum, known only after the symbol
+  // pass.  The pre-pass guesses it: the maximum over symbols 0/1, which for a frame of
+  // constant envelope is the frame's (every noiseless SF7 frame dechirps to 1 + 2^-23 in
+  // both sync windows).  Its estimate is computed on the samples normalised by that guess
+  // (unscaled when the guess is <= 1), exactly as the reference would with that maximum;
+  // stage 2 takes it as the exact estimate when the frame's maximum gives the same scale
+  // (k_cert_split), and the symbol pass's speculation is unaffected either way.
   FrameParams q;
   {
     // LoRaDemod.cpp:79-123 (osr 1: one phase per symbol) for symbol `sym` of the frame
     cf in[P], z[P];
-    gather_points<SF>(a, x + (int64_t)sym * N, l, 1, N, 0, 1, dech, scale, in);
+    gather_points<SF>(a, x + (int64_t)sym * N, l, 1, N, 0, 1, dech, 1.0f, in);
     float mo = 0.0f;  // max(|I|,|Q|) over symbols 0/1 (this group's gathers)
 #pragma unroll
     for (int k = 0; k < P; ++k) mo = amax3(mo, in[k]);
     asm volatile("" : "+v"(mo));
+    const float m01 = frame_max(mo);
+    const int scaled = m01 > 1.0f;
+    const float scale = scaled ? 1.0f / m01 : 1.0f;
+    if (scaled) {
+#pragma unroll
+      for (int k = 0; k < P; ++k) in[k] = cscale(in[k], scale);
+    }
     rotate_place<SF, false>(in, z, 0.0f, 0.0f, a.hann != 0, a.win, l);
     uint64_t key = fft_key<SF, true>(z, row, l, a);
     key = group_max(key, T);
@@ -2247,11 +2257,11 @@ k_est_split(KArgs a, int64_t frames, int rowc) {
 
 // k_cert_split<SF, MODE>: stage 2 of the pipeline (k_est_fast<SF, MODE, 2>'s work) for SF
 // 6-9 in k_est_split's layout: symbols 0 and 1 of a frame on two lane groups side by side.
-// Per frame: the maximum assembled from the pre-pass slot and the data windows' maxima
-// (their loads issued together with the group's symbol gather, which does not depend on
-// it), the exact estimate on the normalised samples (LoRaDemod.cpp:59-135; an unscaled
-// frame's is the pre-pass's, recomputed from identical inputs), the outputs, then the
-// certification of every speculative symbol over the frame's 2T lanes (certify_list).
+// Per frame: the maximum assembled from the pre-pass slot and the data windows' maxima,
+// the exact estimate on the normalised samples (LoRaDemod.cpp:59-135) - the pre-pass's
+// when its guessed scale is the frame's (no samples read), else recomputed - the outputs,
+// then the certification of every speculative symbol over the frame's 2T lanes
+// (certify_list).
 template <int SF, int MODE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
 k_cert_split(KArgs a, int64_t frames, int rowc) {
@@ -2275,11 +2285,9 @@ k_cert_split(KArgs a, int64_t frames, int rowc) {
   const cf* __restrict__ x = a.iq + f * a.frame_stride;
   cf* row = reinterpret_cast<cf*>(smem) + (size_t)g2 * rowc;
   const int per = a.total - 2;
-  // the group's symbol, dechirped (e2e_chain_test.cpp:88-93), not yet normalised
-  cf in[P], z[P];
-  gather_points<SF>(a, x + (int64_t)sym * N, l, 1, N, 0, 1, dech, 1.0f, in);
   // LoRaDemod.cpp:59-67 the frame's maximum: the pre-pass's slot (the samples outside the
   // data windows) and each data window's, over the frame's 2T lanes
+  const FrameParams qg = load_fp(a.fp_spec + f);
   float maxv = l2 == 0 ? __uint_as_float(a.maxbits[f]) : 0.0f;
   {
     const float2* __restrict__ mg = reinterpret_cast<const float2*>(a.spec_marg) + f * a.total + 2;
@@ -2290,27 +2298,31 @@ k_cert_split(KArgs a, int64_t frames, int rowc) {
   }
   const int scaled = maxv > 1.0f;
   const float scale = scaled ? 1.0f / maxv : 1.0f;
-  // LoRaDemod.cpp:68-77 samples * (1/max) after the dechirp (gather_points' order)
-  if (scaled) {
-#pragma unroll
-    for (int q = 0; q < P; ++q) in[q] = cscale(in[q], scale);
-  }
-  // A wave whose frames are all unscaled (max <= 1) takes the pre-pass estimate as it is
-  // (identical inputs and arithmetic); any other computes the exact estimate for all its
-  // frames (an unscaled one's equals the pre-pass's).
-  if (__builtin_amdgcn_readfirstlane(__ballot(scaled) == 0)) {
+  // A frame whose maximum gives the scale the pre-pass guessed (no rescaling either way, or
+  // the same 1/max) has the pre-pass estimate as its exact one: identical inputs and
+  // arithmetic.  A wave of such frames takes it as it is (and reads no samples); any other
+  // computes the exact estimate for all its frames (a guessed frame's equals the pre-pass's).
+  const bool guessed = scaled ? (qg.scaled != 0 && qg.scale == scale) : qg.scaled == 0;
+  if (__builtin_amdgcn_readfirstlane(__ballot(!guessed) == 0)) {
     if (l2 == 0) {
-      const FrameParams qs = load_fp(a.fp_spec + f);
-      store_fp(sp + fg, qs);
+      store_fp(sp + fg, qg);
       if (valid) {
-        store_fp(a.fp + f, qs);
-        if (a.cfo) a.cfo[f] = qs.cfo;
-        if (a.toff) a.toff[f] = qs.toff;
+        store_fp(a.fp + f, qg);
+        if (a.cfo) a.cfo[f] = qg.cfo;
+        if (a.toff) a.toff[f] = qg.toff;
         if (a.max_amp) a.max_amp[f] = maxv;
       }
     }
   } else {
     {
+      // the group's symbol, dechirped (e2e_chain_test.cpp:88-93), then normalised
+      // (LoRaDemod.cpp:68-77, gather_points' order)
+      cf in[P], z[P];
+      gather_points<SF>(a, x + (int64_t)sym * N, l, 1, N, 0, 1, dech, 1.0f, in);
+      if (scaled) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) in[q] = cscale(in[q], scale);
+      }
       // LoRaDemod.cpp:79-123 (osr 1: one phase per symbol) for symbol `sym` of the frame
       rotate_place<SF, false>(in, z, 0.0f, 0.0f, a.hann != 0, a.win, l);
       uint64_t key = fft_key<SF, true>(z, row, l, a);
