@@ -21,6 +21,7 @@ WORK = {
     "awgn0": dict(sf=7, frames=15625, snr_db=0.0),
     "awgn10": dict(sf=7, frames=15625, snr_db=-10.0),
     "osr2": dict(sf=7, frames=15625, osr=2),
+    "osr4": dict(sf=7, frames=15625, osr=4),
     "hann": dict(sf=7, frames=15625, window="hann"),
     "sf12": dict(sf=12, frames=15625),
     "sf12n": dict(sf=12, frames=4000, snr_db=-10.0),
