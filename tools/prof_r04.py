@@ -101,8 +101,9 @@ def main():
                 agg[k].append(e - b)
         out += [f"## {tag}: `python bench.py {'--no-cpu --no-channels --no-fast --no-variants --no-sf12' if key is None else '--sf12-only'}` under rocprofv3 --kernel-trace --stats", "",
                 f"bench.py's HIP-event stage times in the same run (ms per step): estimate stages {stage[1]:.4f}, "
-                f"symbol pass {stage[2]:.4f}; ms_per_step {r['ms_per_step']:.4f} (timed steps replay a HIP graph; "
-                f"the tracer serialises them)", "",
+                f"symbol pass {stage[2]:.4f}; ms_per_step {r['ms_per_step']:.4f} (timed steps: "
+                f"{'one HIP-graph replay' if d.get('config', {}).get('launch') == 'graph' else 'plan.run'} per step; "
+                f"the tracer serialises the kernels)", "",
                 "| kernel | launches | avg us (rocprofv3) |", "|---|---:|---:|"]
         for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
             out.append(f"| `{k}` | {len(v)} | {sum(v) / len(v) / 1e3:.2f} |")
