@@ -198,6 +198,45 @@ def test_mixed_frames_in_one_block(O, amd, sf):
     assert plan.last_kernels() == SPEC
 
 
+@pytest.mark.parametrize("sf", [6, 7, 8, 9])
+def test_scale_guess_holds_and_fails(O, amd, sf):
+    """The SF 6-9 pre-pass normalises symbols 0/1 by their own maximum (k_est_split's scale
+    guess) and stage 2 takes that estimate as the exact one only when the frame's maximum
+    gives the same scale.  Frames of every case side by side, so a stage-2 wave (64 / 2T
+    frames) holds several: the guess holds with max > 1 (noiseless frames that dechirp to
+    1 + 2^-23, and a 1.7 sync peak that is the frame's), it fails because a data window
+    exceeds the sync windows' maximum (both > 1, or sync <= 1 < data), it holds with the
+    whole frame <= 1, and two maxima with the same reciprocal in float (1/m equal, m not)."""
+    rng = np.random.default_rng(500 + sf)
+    N = 1 << sf
+    S = 8
+    base = modulated(O, rng, sf, S, 12, amp=1.0)  # noiseless: max 1 or 1 + ulp everywhere
+    iq = base.copy()
+    iq[1] *= np.float32(1.7)                       # guess holds, scaled
+    iq[2, 5 * N + 3] = np.complex64(3.0 + 0.5j)    # data window above the sync windows' 1 + ulp
+    iq[3] *= np.float32(0.6)                       # whole frame <= 1
+    iq[4] *= np.float32(0.6)
+    iq[4, 6 * N + 11] = np.complex64(0.2 - 1.25j)  # sync <= 1 < data: guess unscaled, frame scaled
+    iq[5] *= np.float32(2.0)
+    ms = np.abs(iq[5, :2 * N].view(np.float32)).max()
+    iq[5, 4 * N + 7] = np.complex64(complex(np.nextafter(ms, np.float32(4.0), dtype=np.float32), 0.0))  # one ulp above
+    # two different maxima whose reciprocals round to the same float: sync max m0, a data
+    # sample m1 > m0 with fl(1/m1) == fl(1/m0) (the reference's inputs are then identical)
+    m0 = np.float32(1.5)
+    for _ in range(10000):
+        m1 = np.nextafter(m0, np.float32(2.0), dtype=np.float32)
+        if np.float32(1.0) / m1 == np.float32(1.0) / m0:
+            break
+        m0 = m1
+    assert np.float32(1.0) / m1 == np.float32(1.0) / m0 and m1 > m0
+    iq[6] = (base[6] / np.float32(np.abs(base[6].view(np.float32)).max()) * np.float32(0.9)).astype(np.complex64)
+    iq[6, 5] = np.complex64(complex(m0, 0.0))          # symbol 0: the sync windows' maximum
+    iq[6, 3 * N + 1] = np.complex64(complex(0.0, m1))  # a data window: the frame's
+    iq[7] = (iq[7] + 0.3 * (rng.standard_normal(S * N) + 1j * rng.standard_normal(S * N))).astype(np.complex64)
+    plan, _ = check(O, amd, iq, sf)
+    assert plan.last_kernels() == SPEC
+
+
 def test_ragged_tail_and_many_frames(O, amd):
     """Frame length not a symbol multiple (the tail is ignored) over 700 frames (many lane
     groups per launch), mixed amplitudes."""

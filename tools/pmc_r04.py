@@ -113,6 +113,24 @@ for wl, (_, sf, frames, S, _), (pv, pg) in zip(WL, WL.values(), (("pmc1", "pmc5"
                         "valu_busy_frac_4cycle": busy4, "valu_packed_share": PK_SHARE[wl],
                         "valu_instr_per_symbol": vi[k] / (frames * (S + 2))})
     lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | {busy4:.3f} | {busy:.3f} |")
+# round 5: the API / RAW lines' symbol pass (k_demod_fast, scalar fp32: no packed
+# instructions in its body), one SQ_INSTS_VALU + GRBM_GUI_ACTIVE pass each (pmc_valu<tag>)
+for wl in ("api_sf7", "raw_sf7"):
+    tag, sf, frames, S, _ = WL[wl]
+    dv = os.path.join(src, f"pmc_valu{tag}")
+    k = summary.get(wl, {}).get("kernel")
+    if not k or not os.path.isdir(dv):
+        continue
+    vi, gr = per_kernel(dv, "SQ_INSTS_VALU"), per_kernel(dv, "GRBM_GUI_ACTIVE")
+    if k not in vi or k not in gr:
+        continue
+    cyc = gr[k] / XCDS
+    busy4 = vi[k] * 4 / (SIMDS * cyc)
+    out_syms = S + 2 if wl.startswith("raw") else S
+    summary[wl].update({"valu_instr_per_launch": vi[k], "gpu_cycles_per_launch": cyc, "valu_busy_frac": busy4,
+                        "valu_busy_frac_4cycle": busy4, "valu_packed_share": 0.0,
+                        "valu_instr_per_symbol": vi[k] / (frames * out_syms)})
+    lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | {busy4:.3f} | {busy4:.3f} |")
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 open(dst, "w").write("\n".join(lines) + "\n")
 json.dump(summary, open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w"), indent=1)

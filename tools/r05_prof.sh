@@ -45,4 +45,13 @@ for cfg in "7:7 none 15625 2" "12:12 none 4000 2" "7o2:7 none 15625 2 64 2" "7o4
   done
 done
 fi
+if [ "${PART:-trace}" = valu ]; then
+# VALU issue of the API / RAW lines' symbol pass (k_demod_fast): SQ_INSTS_VALU with the
+# GPU cycles of the same launches, one pass each
+for cfg in "7api:7 none 15625 2 64 1 api" "7raw:7 none 15625 2 64 1 raw"; do
+  tag=${cfg%%:*}; args=${cfg#*:}
+  echo "== valu $tag $(date +%T)"
+  timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_valu$tag -o run -- python3 tools/prof_workload.py $args > $OUT/pmc_valu$tag.log 2>&1 || { echo "valu pass failed"; tail -3 $OUT/pmc_valu$tag.log; exit 2; }
+done
+fi
 echo "== done $(date +%T)"
