@@ -1441,7 +1441,7 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
     if (e != hipSuccess) rc = set_error(LORA_EIO, "hipMemsetAsync failed");
   }
   // Speculative single-read pipeline (LoRaDemod.cpp:59-192 reordered, results identical;
-  // LEGACY frames at osr 1-4, either window):
+  // LEGACY frames at osr 1-4, either window; API frames at osr 1, below):
   //   1. offset estimate on UNSCALED samples (k_est_split / k_est_fast<SPEC=1>), plus the
   //      maximum of the samples outside the data-symbol windows it implies;
   //   2. every symbol with those offsets on unscaled samples (k_spec_demod), which also
@@ -1460,12 +1460,20 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   // Oversampled frames (osr 2-4) take it too: the symbol pass reads every sample of each
   // window (the frame maximum) and transforms every osr-th one; its buffer offsets need the
   // frame's bytes below 2^31.
-  const bool spec_ok = plan->spec && p.mode == LORA_MODE_LEGACY && p.osr >= 1 && p.osr <= 4 && p.sf >= 6 &&
-                       total >= 3 && total - 2 <= lora::kSpecChunks * (plan->N / 16) &&
+  // LORA_MODE_API frames at osr 1 take it too (phy.cpp:178-239): no normalisation, so the
+  // exact estimate runs first and the symbol pass speculates only on the rotation (the
+  // hardware sine/cosine and fused multiply-adds), certified with no rate difference.
+  const bool api = p.mode == LORA_MODE_API;
+  const bool spec_ok = plan->spec && (p.mode == LORA_MODE_LEGACY || (api && p.osr == 1)) && p.osr >= 1 &&
+                       p.osr <= 4 && p.sf >= 6 && total >= 3 && total - 2 <= lora::kSpecChunks * (plan->N / 16) &&
                        sync_frames * frame_stride * 8 < (int64_t(1) << 31) && frame_len * 8 < (int64_t(1) << 31);
   if (rc == LORA_OK && spec_ok) {
     KArgs as = a;
     as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows
+    if (api) {
+      as.fp_spec = as.fp;  // the offsets the symbol pass uses are the exact ones
+      as.dechirp = 1;      // each window times the down-chirp (table phase 0, k_spec_demod API)
+    }
     bool ok;
     {
       ProfScope ps(plan, 1, st);

@@ -1043,7 +1043,11 @@ k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
 // sample (LoRaDemod.cpp:59-67) - the frame is still read once.  OSRV 2 / 4: osr known at
 // compile time, a point's osr samples in one / two 16-byte loads; OSRV 0: a.osr at run time
 // (osr 3, and the Hann window), one 8-byte load per sample.
-template <int SF, int MODE, bool HANN = false, int OSRV = 1>
+// API (LORA_MODE_API at osr 1, lora_capi.hip): each window times the down-chirp from table
+// phase 0 (phy.cpp:211-225 multiplies sym[i] by a fresh down-chirp's [i]) with the exact
+// offsets, no sync blocks (the estimate kernel demodulated symbols 0/1 exactly), and the
+// reject list's counters zeroed here (no pre-pass runs).
+template <int SF, int MODE, bool HANN = false, int OSRV = 1, bool API = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   using G = Geo<SF>;
@@ -1072,6 +1076,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   constexpr bool DTAB = DTL && spec_dtab<SF>();
   float4* dtl = reinterpret_cast<float4*>(smem + spec_dtl_offset<SF>());
   cf* dtab = reinterpret_cast<cf*>(smem + spec_dtl_offset<SF>());
+  if (API && blockIdx.x == 0 && threadIdx.x < kFixStripes) a.fix_count[16 * threadIdx.x] = 0;
   if constexpr (NTW > 0) {
     const int tid = threadIdx.x;
     if (tid < NTW) twl[tid] = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
@@ -1085,7 +1090,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   }
   const int bpf = (per + SPB - 1) / SPB;  // data blocks per frame
   const int64_t dblocks = frames * bpf;
-  const int64_t blocks = dblocks + (2 * frames + SPB - 1) / SPB;
+  const int64_t blocks = dblocks + (API ? 0 : (2 * frames + SPB - 1) / SPB);
   const int64_t groups = (blocks + BPG - 1) / BPG;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   typedef float v2f __attribute__((ext_vector_type(2)));
@@ -1127,6 +1132,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
     int64_t base;
     int cg;
     sym_base(s, step, a.frame_len, toff, base, cg);
+    if constexpr (API) cg = 0;
     cf in[P];
     float pm = 0.0f;
     int lr = l;
@@ -1308,6 +1314,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       B.toff = fps[B.f].t_off;
       int64_t base;
       sym_base(B.s, N, a.frame_len, B.toff, base, B.cg);
+      if constexpr (API) B.cg = 0;
       B.d = (int)(base & (D - 1));
       B.mis = __builtin_amdgcn_readfirstlane(__ballot(B.d != 0) != 0);
       const __amdgpu_buffer_rsrc_t rx =
@@ -1453,6 +1460,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       B.toff = fps[B.f].t_off;
       int64_t base;
       sym_base(B.s, N, a.frame_len, B.toff, base, B.cg);
+      if constexpr (API) B.cg = 0;
       B.d = (int)(base & (D - 1));
       B.mis = __builtin_amdgcn_readfirstlane(__ballot(l < B.d) != 0);  // waves holding late lanes
       const __amdgpu_buffer_rsrc_t rx =
@@ -1652,7 +1660,7 @@ __device__ __forceinline__ void certify_list(const KArgs& a, int64_t f, const Fr
   // the sync symbols (entries 0, 1: margin, index) on lanes 0 and 1: their windows lie in
   // [0, 2N + t_off), whose maximum the pre-pass took (a.maxbits[f] <= maxv)
   bool sync_rej = false;
-  {
+  if (a.mode != LORA_MODE_API) {  // (API: the estimate kernel demodulated symbols 0/1 exactly)
     const uint2 e = mg[li < 2 ? li : 0];
     const bool ok = certified((double)__uint_as_float(e.x), (double)__uint_as_float(a.maxbits[f]), li & 1);
     const uint32_t ok1 = (uint32_t)__shfl_down((int)ok, 1, 64), i1 = (uint32_t)__shfl_down((int)e.y, 1, 64);
@@ -2460,26 +2468,26 @@ int device_cus() {
   return cache[dev];
 }
 
-template <int SF, int MODE, bool HANN, int OSRV>
+template <int SF, int MODE, bool HANN, int OSRV, bool API = false>
 bool launch_spec_demod_w(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
   const size_t lds = spec_lds_bytes<SF>();
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN, OSRV>,
+    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN, OSRV, API>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return false;
   // the kernel's blocks: SPB symbols of one frame (see k_spec_demod), BPG per workgroup round
   constexpr int SPB = G::WAVE_LOCAL ? 64 / G::T : G::SPW, BPG = G::WAVE_LOCAL ? 4 : 1;
   const int per = a.total - 2;
-  const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB) + (2 * frames + SPB - 1) / SPB;
+  const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB) + (API ? 0 : (2 * frames + SPB - 1) / SPB);
   const int64_t groups = (blocks + BPG - 1) / BPG;
   // persistent: the wave-local geometries, and every prefetching one (PF3: SF 10-12)
   const bool persist = G::WAVE_LOCAL || (G::NPASS == 3 && a.osr == 1);
   const int64_t cap = persist ? (int64_t)device_cus() * kSpecWgPerCu : groups;
   const int64_t grid = groups < cap ? groups : cap;
-  launch(k_spec_demod<SF, MODE, HANN, OSRV>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
+  launch(k_spec_demod<SF, MODE, HANN, OSRV, API>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
   return true;
 }
 // the Hann window (LoRaDemod.cpp:158-160) and oversampling as instantiations of their own:
@@ -2521,6 +2529,17 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   if constexpr (SF < 6) {
     return false;
   } else {
+    if (a.mode == LORA_MODE_API) {
+      // lora_phy::demodulate (osr 1): the exact estimate with the sync word (the three-launch
+      // path's kernel), the symbol pass with the exact offsets (down-chirp from table phase
+      // 0, no sync blocks), the certification with no rate difference, the recompute
+      if (stage == 0) return launch_est_mode<SF, 2, 0>(a, frames, st);
+      if (stage == 1)
+        return a.hann ? launch_spec_demod_w<SF, 0, true, 1, true>(a, frames, st)
+                      : launch_spec_demod_w<SF, 0, false, 1, true>(a, frames, st);
+      if (stage == 2) return launch_est_mode<SF, 2, 2>(a, frames, st);
+      return launch_spec_fix<SF, 2>(a, frames, st);
+    }
     if (a.osr > 1) {  // oversampled frames: the estimate stages at run-time osr (MODE 2)
       if (stage == 0) return launch_est_mode<SF, 2, 1>(a, frames, st);
       if (stage == 1)

@@ -94,7 +94,7 @@ def dynamic_lds(demangled):
     # the modulator, frame-max and compensation kernels use static LDS only
     if re.match(r"void (k_mod_\w+|k_frame_max\w*|k_compensate)\b", demangled):
         return 0
-    m = re.match(r"void (k_\w+)<(\d+)(?:, (\w+))?(?:, (\w+))?(?:, (\w+))?>", demangled)
+    m = re.match(r"void (k_\w+)<(\d+)(?:, (\w+))?(?:, (\w+))?(?:, (\w+))?(?:, (\w+))?>", demangled)
     if not m or int(m.group(2)) < 6 or int(m.group(2)) > 12:
         return None
     k, sf = m.group(1), int(m.group(2))

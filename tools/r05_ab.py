@@ -22,6 +22,8 @@ WORK = {
     "awgn10": dict(sf=7, frames=15625, snr_db=-10.0),
     "osr2": dict(sf=7, frames=15625, osr=2),
     "osr4": dict(sf=7, frames=15625, osr=4),
+    "api": dict(sf=7, frames=15625, mode="api"),
+    "api12": dict(sf=12, frames=4000, mode="api"),
     "hann": dict(sf=7, frames=15625, window="hann"),
     "sf12": dict(sf=12, frames=15625),
     "sf12n": dict(sf=12, frames=4000, snr_db=-10.0),
