@@ -183,7 +183,9 @@ int lora_demod_last_kernels(const lora_demod_plan* plan);
 /* LEGACY frames at osr 1-4 with either window (none or Hann), SF 6-12, of 3 .. 2 + 4 * 2^SF symbols (SF7: 514),
  * run as a speculative single-read pipeline (LORA_KERNEL_SPEC) - and LORA_MODE_API frames at osr 1 (the exact
  * estimate first, then every data symbol rotated with the hardware sine/cosine and certified or recomputed
- * exactly; phy.cpp:178-239): the offset estimate on unscaled samples, every
+ * exactly; phy.cpp:178-239) and LORA_MODE_RAW frames at osr 1, SF 6-9 (every symbol through the same symbol
+ * pass with no rotation, certified against the transforms' rounding or recomputed): the offset estimate on
+ * unscaled samples, every
  * data symbol demodulated once while the frame maximum is reduced from the same read, then
  * the exact estimate, with each data symbol either certified by a rounding bound on its
  * argmax margin or recomputed exactly - the outputs equal the reference's (LoRaDemod.cpp:

@@ -160,6 +160,9 @@ WsLayout ws_layout(int64_t frames, int64_t frame_len, int step, int N) {
   const int64_t spb = lora::est_frames_per_block(N);
   const int64_t wgs = (frames + spb - 1) / spb;
   w.fix_cap = (wgs + lora::kFixStripes - 1) / lora::kFixStripes * spb * (per + 1);
+  // (LORA_MODE_RAW's certification lists from blocks of 256 symbols, every symbol an entry)
+  const int64_t rblocks = (frames * total + 255) / 256;
+  w.fix_cap = std::max<int64_t>(w.fix_cap, (rblocks + lora::kFixStripes - 1) / lora::kFixStripes * 256);
   w.total = w.fix + al(64 * lora::kFixStripes + (size_t)lora::kFixStripes * w.fix_cap * 2 * sizeof(uint32_t));
   return w;
 }
@@ -1467,7 +1470,30 @@ int64_t lora_demod_batch(lora_demod_plan* plan, const float* iq, int64_t frames,
   const bool spec_ok = plan->spec && (p.mode == LORA_MODE_LEGACY || (api && p.osr == 1)) && p.osr >= 1 &&
                        p.osr <= 4 && p.sf >= 6 && total >= 3 && total - 2 <= lora::kSpecChunks * (plan->N / 16) &&
                        sync_frames * frame_stride * 8 < (int64_t(1) << 31) && frame_len * 8 < (int64_t(1) << 31);
-  if (rc == LORA_OK && spec_ok) {
+  // LORA_MODE_RAW at osr 1, SF 6-9 (the detector alone, awgn_sweep.py:262-273): every symbol through
+  // the symbol pass with no offsets and no rotation, certified against the transforms'
+  // rounding alone (k_cert_raw) or recomputed exactly (k_spec_fix)
+  const bool spec_raw = plan->spec && p.mode == LORA_MODE_RAW && p.osr == 1 && p.sf >= 6 && p.sf <= 9 && total >= 1 &&
+                        total <= lora::kSpecChunks * (plan->N / 16) && frame_len * 8 < (int64_t(1) << 31);
+  if (rc == LORA_OK && spec_raw) {
+    KArgs as = a;
+    hipError_t e = hipMemsetAsync(a.fp, 0, sizeof(lora::FrameParams) * (size_t)frames, st);  // no offsets
+    bool ok = e == hipSuccess;
+    if (ok) {
+      ProfScope ps(plan, 2, st);
+      ok = lora::launch_spec(as, frames, 1, st);
+    }
+    if (ok) {
+      ProfScope ps(plan, 1, st);
+      ok = lora::launch_spec(as, frames, 2, st);
+    }
+    if (ok) {
+      ProfScope ps(plan, 1, st);
+      ok = lora::launch_spec(as, frames, 3, st);
+    }
+    if (!ok) rc = set_error(LORA_EIO, "RAW pipeline launch failed");
+    kernels |= LORA_KERNEL_SPEC | LORA_KERNEL_DEMOD;
+  } else if (rc == LORA_OK && spec_ok) {
     KArgs as = a;
     as.mx_bpf = 1;  // one slot per frame: the pre-pass's max outside the data windows
     if (api) {

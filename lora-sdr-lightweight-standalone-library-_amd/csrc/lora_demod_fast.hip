@@ -1043,11 +1043,13 @@ k_demod_fast(KArgs a, int s0, int64_t work, int rowc) {
 // sample (LoRaDemod.cpp:59-67) - the frame is still read once.  OSRV 2 / 4: osr known at
 // compile time, a point's osr samples in one / two 16-byte loads; OSRV 0: a.osr at run time
 // (osr 3, and the Hann window), one 8-byte load per sample.
-// API (LORA_MODE_API at osr 1, lora_capi.hip): each window times the down-chirp from table
-// phase 0 (phy.cpp:211-225 multiplies sym[i] by a fresh down-chirp's [i]) with the exact
-// offsets, no sync blocks (the estimate kernel demodulated symbols 0/1 exactly), and the
-// reject list's counters zeroed here (no pre-pass runs).
-template <int SF, int MODE, bool HANN = false, int OSRV = 1, bool API = false>
+// SPM (lora_capi.hip) 1 = API (LORA_MODE_API at osr 1): each window times the down-chirp
+// from table phase 0 (phy.cpp:211-225 multiplies sym[i] by a fresh down-chirp's [i]) with the
+// exact offsets, no sync blocks (the estimate kernel demodulated symbols 0/1 exactly); 2 =
+// RAW (LORA_MODE_RAW at osr 1, the detector alone, LoRaDetector.hpp:39-58): every symbol of
+// the frame an output at t_off 0 with no rotation (the factors of rate 0 are exactly 1).
+// Both zero the reject list's counters here (no pre-pass runs).
+template <int SF, int MODE, bool HANN = false, int OSRV = 1, int SPM = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(demod_waves_per_eu<SF>())))
 k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   using G = Geo<SF>;
@@ -1068,7 +1070,9 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   cf* rows = reinterpret_cast<cf*>(smem);
   cf* twl = rows + (size_t)SPW * rowc;
   const int tot = a.total;
-  const int per = tot - 2;
+  constexpr bool API = SPM == 1, RAWM = SPM == 2;
+  constexpr int S0 = RAWM ? 0 : 2;  // the frame's first output symbol
+  const int per = tot - S0;
   // (PF geometries, MODE 0) the dechirp table's pairs at table phase 0 - what every window
   // of a t_off = 0 frame reads - staged after the twiddles: dtl[p T + c] = downP[p (N + T) + c]
   constexpr bool DTL = WL && G::NPASS == 2 && !OSRN && MODE == 0;
@@ -1076,7 +1080,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   constexpr bool DTAB = DTL && spec_dtab<SF>();
   float4* dtl = reinterpret_cast<float4*>(smem + spec_dtl_offset<SF>());
   cf* dtab = reinterpret_cast<cf*>(smem + spec_dtl_offset<SF>());
-  if (API && blockIdx.x == 0 && threadIdx.x < kFixStripes) a.fix_count[16 * threadIdx.x] = 0;
+  if (SPM != 0 && blockIdx.x == 0 && threadIdx.x < kFixStripes) a.fix_count[16 * threadIdx.x] = 0;
   if constexpr (NTW > 0) {
     const int tid = threadIdx.x;
     if (tid < NTW) twl[tid] = a.twTA ? a.twTA[tid] : a.tw[twT_index(N, G::MA_A, tid / G::MA_A, tid % G::MA_A)];
@@ -1090,7 +1094,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   }
   const int bpf = (per + SPB - 1) / SPB;  // data blocks per frame
   const int64_t dblocks = frames * bpf;
-  const int64_t blocks = dblocks + (API ? 0 : (2 * frames + SPB - 1) / SPB);
+  const int64_t blocks = dblocks + (SPM != 0 ? 0 : (2 * frames + SPB - 1) / SPB);
   const int64_t groups = (blocks + BPG - 1) / BPG;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   typedef float v2f __attribute__((ext_vector_type(2)));
@@ -1114,7 +1118,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       f = fu = fb;
       const int jl = rb * SPB + gi;
       valid = jl < per;
-      s = 2 + (valid ? jl : per - 1);  // a partial block's spare slots mirror a valid symbol
+      s = S0 + (valid ? jl : per - 1);  // a partial block's spare slots mirror a valid symbol
     } else {
       const int64_t k0 = (b - dblocks) * SPB;
       int64_t k = k0 + gi;
@@ -1125,9 +1129,9 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       fu = k0 >> 1;
       rel = (int)((f - fu) * a.frame_stride * 8);  // < 2^31: lora_demod_batch checks the stride
     }
-    const FrameParams fp = a.fp_spec[f];
-    const float rate = fp.rate;
-    const int toff = fp.t_off;
+    const FrameParams fp = RAWM ? FrameParams{} : a.fp_spec[f];
+    const float rate = RAWM ? 0.0f : fp.rate;
+    const int toff = RAWM ? 0 : fp.t_off;
     const int step = OSRN ? a.step : N;
     int64_t base;
     int cg;
@@ -1268,7 +1272,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       const float margin = __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec));
       uint2* mg = reinterpret_cast<uint2*>(a.spec_marg) + f * tot + s;
       if constexpr (!SYNC) {
-        if (lbest == best && a.syms) a.syms[f * a.sym_stride + (s - 2)] = (uint16_t)idx;
+        if (lbest == best && a.syms) a.syms[f * a.sym_stride + (s - S0)] = (uint16_t)idx;
         if (l == 0) *mg = make_uint2(__float_as_uint(margin), __float_as_uint(pm));
       } else {
         if (lbest == best) *mg = make_uint2(__float_as_uint(margin), idx);
@@ -1309,9 +1313,9 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       B.f = bb / bpf;
       const int jl = (int)(bb - B.f * bpf) * SPB + gi;
       B.valid = jl < per;
-      B.s = 2 + (B.valid ? jl : per - 1);
-      B.rate = fps[B.f].rate;  // scalar loads (constant address space, uniform frame)
-      B.toff = fps[B.f].t_off;
+      B.s = S0 + (B.valid ? jl : per - 1);
+      B.rate = RAWM ? 0.0f : fps[B.f].rate;  // scalar loads (constant address space, uniform frame)
+      B.toff = RAWM ? 0 : fps[B.f].t_off;
       int64_t base;
       sym_base(B.s, N, a.frame_len, B.toff, base, B.cg);
       if constexpr (API) B.cg = 0;
@@ -1419,7 +1423,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
         const int o = (int)(best & 15u);
         const uint32_t idx = (uint32_t)(lr + T * (o % NG) + ML * (o / NG));
         const float margin = __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec));
-        if (lbest == best && a.syms) a.syms[B.f * a.sym_stride + (B.s - 2)] = (uint16_t)idx;
+        if (lbest == best && a.syms) a.syms[B.f * a.sym_stride + (B.s - S0)] = (uint16_t)idx;
         if (l == 0)
           reinterpret_cast<uint2*>(a.spec_marg)[B.f * tot + B.s] = make_uint2(__float_as_uint(margin), __float_as_uint(pm));
       }
@@ -1455,9 +1459,9 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       B.f = bb / bpf;
       const int jl = (int)(bb - B.f * bpf) * SPB + gi;
       B.valid = jl < per;
-      B.s = 2 + (B.valid ? jl : per - 1);
-      B.rate = fps[B.f].rate;
-      B.toff = fps[B.f].t_off;
+      B.s = S0 + (B.valid ? jl : per - 1);
+      B.rate = RAWM ? 0.0f : fps[B.f].rate;
+      B.toff = RAWM ? 0 : fps[B.f].t_off;
       int64_t base;
       sym_base(B.s, N, a.frame_len, B.toff, base, B.cg);
       if constexpr (API) B.cg = 0;
@@ -1543,7 +1547,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
         const uint32_t idx = (uint32_t)(lr + T * (o % NG) + ML * (o / NG));
         const float margin =
             __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec));
-        if (lbest == best && a.syms) a.syms[B.f * a.sym_stride + (B.s - 2)] = (uint16_t)idx;
+        if (lbest == best && a.syms) a.syms[B.f * a.sym_stride + (B.s - S0)] = (uint16_t)idx;
         if (l == 0)
           reinterpret_cast<uint2*>(a.spec_marg)[B.f * tot + B.s] = make_uint2(__float_as_uint(margin), __float_as_uint(pm));
       }
@@ -2058,6 +2062,62 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
   }
 }
 
+// The certification test of one speculative symbol s (certify_list's, derivation at
+// k_est_fast<SPEC = 2>) for a frame whose exact and speculative rates are rmax apart by
+// drate, |t_off| = tabs.
+template <int SF>
+__device__ __forceinline__ bool spec_certified(double d, double wmax, int s, double rmax, double drate, double tabs) {
+  constexpr int N = 1 << SF;
+  constexpr int T = N >= 16 ? N / 16 : 1;
+  const double u = 1.0 / 16777216.0;
+  const double E = (8.0 * SF + 42.0) * u;
+  const double e_spec = 33.0 * u * rmax * T + 16.0 * (1.87e-7 + 1.4143 * kHwSinCosErr) + 2.6e-6 + 9.6e-7;
+  const double n1 = 2.0 * N * wmax;
+  const double L = (double)(s + 1) * N + tabs;
+  const double e_ref = u * rmax * (L + 2.0 * N);
+  const double B = n1 * (drate * N + e_ref + e_spec + 2.0 * E);
+  return d > 4.0 * B + 0x1p-60;
+}
+
+// Appends the wave's lanes with `rej` set to the reject list as (f, code): one returning
+// atomic per wave on the workgroup's stripe (wave-uniform call).
+__device__ __forceinline__ void fix_list_append(const KArgs& a, bool rej, int64_t f, uint32_t code) {
+  const uint64_t m = __ballot(rej);
+  if (m) {  // wave-uniform
+    const int lane = (int)__lane_id();
+    const int first = __builtin_ctzll(m);
+    const int stripe = (int)(blockIdx.x % kFixStripes);
+    unsigned base = 0;
+    if (lane == first) base = atomicAdd(a.fix_count + 16 * stripe, (unsigned)__popcll(m));
+    base = (unsigned)__shfl((int)base, first, 64);
+    if (rej) {
+      const size_t slot = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
+      uint32_t* list = a.fix_list + 2 * (size_t)stripe * (size_t)a.fix_cap;
+      list[2 * slot] = (uint32_t)f;
+      list[2 * slot + 1] = code;
+    }
+  }
+}
+
+// k_cert_raw: the certification of LORA_MODE_RAW's symbol pass (k_spec_demod SPM 2), one
+// thread per symbol: no offsets, no rotation (its factors are exactly 1), no rescaling, so
+// only the transforms' rounding bounds the argmax margin (spec_certified with rate 0); the
+// rejected symbols are listed for k_spec_fix.
+template <int SF>
+__global__ void __launch_bounds__(256) k_cert_raw(KArgs a, int64_t frames) {
+  const int tot = a.total;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = i < frames * tot;
+  const int64_t f = valid ? i / tot : 0;
+  const int s = valid ? (int)(i - f * tot) : 0;
+  bool rej = false;
+  if (valid) {
+    const uint2 e = reinterpret_cast<const uint2*>(a.spec_marg)[f * tot + s];
+    rej = !spec_certified<SF>((double)__uint_as_float(e.x), (double)__uint_as_float(e.y), s, 0.0, 0.0, 0.0);
+  }
+  fix_list_append(a, rej, f, (uint32_t)s);
+}
+
 // k_spec_fix: the pipeline's fourth launch.  Every data symbol the certification
 // rejected (k_est_fast<SPEC = 2>'s list: frame, data symbol) recomputed exactly with the
 // frame's exact offsets a.fp[f] (LoRaDemod.cpp:137-175), and every rejected sync word
@@ -2107,12 +2167,14 @@ k_spec_fix(KArgs a, int rowc, int64_t grid) {
     // the lane index opaque per entry (k_est_fast: no lane addresses hoisted out of the loop)
     int lo = l;
     asm volatile("" : "+v"(lo));
-    const uint32_t i0 = exact_symbol<SF, MODE>(a, x, q, sync ? 0 : 2 + (int)j, row, lo, tid, red);
+    // (LORA_MODE_RAW: entry j is the frame's symbol j itself, every symbol an output)
+    const int js = (a.mode == LORA_MODE_RAW ? 0 : 2) + (int)j;
+    const uint32_t i0 = exact_symbol<SF, MODE>(a, x, q, sync ? 0 : js, row, lo, tid, red);
     // a second transform when any group of the workgroup holds a sync entry (uniform, so
     // the transform's barriers match); the others repeat theirs
     const bool any_sync = G::WAVE_LOCAL ? __any(sync) : __syncthreads_or(sync);
     uint32_t i1 = 0;
-    if (any_sync) i1 = exact_symbol<SF, MODE>(a, x, q, sync ? 1 : 2 + (int)j, row, lo, tid, red);
+    if (any_sync) i1 = exact_symbol<SF, MODE>(a, x, q, sync ? 1 : js, row, lo, tid, red);
     if (l == 0 && valid) {
       if (!sync) {
         if (a.syms) a.syms[f * a.sym_stride + j] = (uint16_t)i0;
@@ -2468,26 +2530,26 @@ int device_cus() {
   return cache[dev];
 }
 
-template <int SF, int MODE, bool HANN, int OSRV, bool API = false>
+template <int SF, int MODE, bool HANN, int OSRV, int SPM = 0>
 bool launch_spec_demod_w(const KArgs& a, int64_t frames, hipStream_t st) {
   using G = Geo<SF>;
   const int rowc = row_complex<SF>();
   const size_t lds = spec_lds_bytes<SF>();
   if (lds > 160 * 1024) return false;
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN, OSRV, API>,
+    if (hipFuncSetAttribute((const void*)k_spec_demod<SF, MODE, HANN, OSRV, SPM>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
       return false;
   // the kernel's blocks: SPB symbols of one frame (see k_spec_demod), BPG per workgroup round
   constexpr int SPB = G::WAVE_LOCAL ? 64 / G::T : G::SPW, BPG = G::WAVE_LOCAL ? 4 : 1;
-  const int per = a.total - 2;
-  const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB) + (API ? 0 : (2 * frames + SPB - 1) / SPB);
+  const int per = a.total - (SPM == 2 ? 0 : 2);
+  const int64_t blocks = frames * (int64_t)((per + SPB - 1) / SPB) + (SPM != 0 ? 0 : (2 * frames + SPB - 1) / SPB);
   const int64_t groups = (blocks + BPG - 1) / BPG;
   // persistent: the wave-local geometries, and every prefetching one (PF3: SF 10-12)
   const bool persist = G::WAVE_LOCAL || (G::NPASS == 3 && a.osr == 1);
   const int64_t cap = persist ? (int64_t)device_cus() * kSpecWgPerCu : groups;
   const int64_t grid = groups < cap ? groups : cap;
-  launch(k_spec_demod<SF, MODE, HANN, OSRV, API>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
+  launch(k_spec_demod<SF, MODE, HANN, OSRV, SPM>, dim3((unsigned)grid), dim3(256), lds, st, a, frames, rowc, grid);
   return true;
 }
 // the Hann window (LoRaDemod.cpp:158-160) and oversampling as instantiations of their own:
@@ -2529,14 +2591,37 @@ bool launch_spec_sf(const KArgs& a, int64_t frames, int stage, hipStream_t st) {
   if constexpr (SF < 6) {
     return false;
   } else {
+    if (a.mode == LORA_MODE_RAW) {
+      // the detector alone (osr 1, SF 6-9: at SF 10-12 this instantiation spills): the symbol
+      // pass over every symbol, its certification, the recompute (the frame parameters are
+      // zero: no offsets, no rescaling)
+      if constexpr (SF > 9) {
+        return false;
+      } else {
+        if (stage == 1) {
+          if (a.hann)
+            return a.dechirp ? launch_spec_demod_w<SF, 0, true, 1, 2>(a, frames, st)
+                             : launch_spec_demod_w<SF, 1, true, 1, 2>(a, frames, st);
+          return a.dechirp ? launch_spec_demod_w<SF, 0, false, 1, 2>(a, frames, st)
+                           : launch_spec_demod_w<SF, 1, false, 1, 2>(a, frames, st);
+        }
+        if (stage == 2) {
+          const int64_t n = frames * (int64_t)a.total;
+          launch(k_cert_raw<SF>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, frames);
+          return true;
+        }
+        if (stage == 3) return launch_spec_fix<SF, 2>(a, frames, st);
+        return false;
+      }
+    }
     if (a.mode == LORA_MODE_API) {
       // lora_phy::demodulate (osr 1): the exact estimate with the sync word (the three-launch
       // path's kernel), the symbol pass with the exact offsets (down-chirp from table phase
       // 0, no sync blocks), the certification with no rate difference, the recompute
       if (stage == 0) return launch_est_mode<SF, 2, 0>(a, frames, st);
       if (stage == 1)
-        return a.hann ? launch_spec_demod_w<SF, 0, true, 1, true>(a, frames, st)
-                      : launch_spec_demod_w<SF, 0, false, 1, true>(a, frames, st);
+        return a.hann ? launch_spec_demod_w<SF, 0, true, 1, 1>(a, frames, st)
+                      : launch_spec_demod_w<SF, 0, false, 1, 1>(a, frames, st);
       if (stage == 2) return launch_est_mode<SF, 2, 2>(a, frames, st);
       return launch_spec_fix<SF, 2>(a, frames, st);
     }

@@ -441,3 +441,48 @@ def test_api_mode_through_the_pipeline(O, amd, sf, hann, snr_db):
             assert int(res.sync[f]) == osync
             assert bits(res.cfo[f].item()) == bits(ocfo)
             assert bits(res.time_offset[f].item()) == bits(otoff)
+
+
+@pytest.mark.parametrize("sf", [6, 7, 8, 9])
+@pytest.mark.parametrize("hann", [False, True])
+@pytest.mark.parametrize("dechirp", [True, False])
+def test_raw_mode_through_the_pipeline(O, amd, sf, hann, dechirp):
+    """LORA_MODE_RAW (the detector alone, awgn_sweep.py:262-273) at osr 1, SF 6-9 takes the
+    pipeline: every symbol of the frame through the symbol pass (no offsets, no rotation),
+    certified against the transforms' rounding alone (k_cert_raw) or recomputed exactly.
+    Frames from noiseless to -15 dB (many near-ties), two exact equal-power ties and a
+    ragged tail; every symbol equal to the reference's detector, and to the three-launch
+    path."""
+    rng = np.random.default_rng(900 + 10 * sf + 2 * hann + dechirp)
+    N = 1 << sf
+    F, S = 8, 9
+    L = S * N + 5
+    rows = []
+    for f in range(F):
+        syms = rng.integers(0, N, S - 2).astype(np.uint16)
+        x = O.lora_modulate(syms, sf, 1, 125000, 1.0, 0x12)
+        if not dechirp:
+            x = O.dechirp(x, sf, 1)
+        x = np.concatenate([x, np.zeros(5, np.complex64)])
+        sig = [0.0, 0.3, 1.0, 3.0, 4.0, 0.0, 0.5, 2.0][f]
+        x = (x + sig * (rng.standard_normal(L) + 1j * rng.standard_normal(L))).astype(np.complex64)
+        rows.append(x)
+    iq = np.stack(rows)
+    # two symbols of frame 5 with two bins of exactly equal power (dechirped domain)
+    if not dechirp:
+        for s in (3, 6):
+            iq[5, s * N:(s + 1) * N] = tone(N, 5 + s, 1.3) + tone(N, N // 2 + s, 1.3, 0.7)
+    for spec in (True, False):
+        with amd.spec_pipeline(spec):
+            plan = amd.DemodPlan(sf, 1, 125000, "hann" if hann else "none", dechirp=dechirp, mode="raw")
+        res = plan.run(torch.from_numpy(iq).cuda())
+        torch.cuda.synchronize()
+        assert ("spec" in plan.last_kernels()) == spec
+        got = res.symbols.cpu().numpy()
+        assert got.shape == (F, S)
+        for f in range(F):
+            np.testing.assert_array_equal(got[f], O.raw_demod(iq[f], sf, 1, hann, dechirp=dechirp),
+                                          err_msg=f"spec={spec} frame {f}")
+        assert int(res.sync.to(torch.int32).sum()) == 0 and float(res.cfo.abs().sum()) == 0.0
+        if spec and not dechirp:
+            assert plan.spec_recomputed() > 0  # the ties at least

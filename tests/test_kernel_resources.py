@@ -40,19 +40,22 @@ def kernels():
 # (kernel, max VGPRs): the speculative pipeline of the bench workloads (SF7, SF12, osr 2, API)
 PIPELINE = [
     ("k_est_split<7, 0>", 128),
-    ("k_spec_demod<7, 0, false, 1, false>", 128),
+    ("k_spec_demod<7, 0, false, 1, 0>", 128),
     ("k_cert_split<7, 0>", 128),
     ("k_spec_fix<7, 0>", 256),
     ("k_est_fast<12, 0, 1>", 128),
-    ("k_spec_demod<12, 0, false, 1, false>", 128),
+    ("k_spec_demod<12, 0, false, 1, 0>", 128),
     ("k_est_fast<12, 0, 2>", 128),
     ("k_spec_fix<12, 0>", 256),
     ("k_est_fast<7, 2, 1>", 256),
-    ("k_spec_demod<7, 0, false, 2, false>", 128),
+    ("k_spec_demod<7, 0, false, 2, 0>", 128),
     ("k_est_fast<7, 2, 2>", 256),
     # the API line (LORA_MODE_API through the pipeline): exact estimate, symbol pass, stage 2
     ("k_est_fast<7, 2, 0>", 256),
-    ("k_spec_demod<7, 0, false, 1, true>", 128),
+    ("k_spec_demod<7, 0, false, 1, 1>", 128),
+    # the RAW line (the detector alone through the pipeline)
+    ("k_spec_demod<7, 0, false, 1, 2>", 128),
+    ("k_cert_raw<7>", 128),
 ]
 
 

@@ -23,6 +23,7 @@ WORK = {
     "osr2": dict(sf=7, frames=15625, osr=2),
     "osr4": dict(sf=7, frames=15625, osr=4),
     "api": dict(sf=7, frames=15625, mode="api"),
+    "raw": dict(sf=7, frames=15625, mode="raw"),
     "api12": dict(sf=12, frames=4000, mode="api"),
     "hann": dict(sf=7, frames=15625, window="hann"),
     "sf12": dict(sf=12, frames=15625),
