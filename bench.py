@@ -280,9 +280,12 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     # window of the frame read once, one index written per data symbol)
     spec = "spec" in kernels
     W = 8 * N * osr  # bytes per symbol window
+    # (API: the pass reads the data windows only - the estimate kernel demodulates symbols
+    # 0/1; RAW: every window, every symbol an output)
+    spec_windows = data_syms if mode == "api" else total_syms
     dom_bytes = {0: frames * total_syms * W,                 # frame max: the whole IQ
                  1: frames * (2 * W + 9),                     # estimate: symbols 0/1 + outputs
-                 2: (frames * (total_syms * W + 2 * data_syms) if spec
+                 2: (frames * (spec_windows * W + 2 * out_syms) if spec
                      # three-launch demod: every osr-th sample of a window is read
                      else frames * out_syms * (8 * N + 2))}[dom]
     dom_gbs = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9

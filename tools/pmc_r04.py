@@ -56,7 +56,11 @@ for wl, (tag, sf, frames, S, osr) in WL.items():
     # u16 index per data symbol; the three-launch demod (API / RAW lines) reads and writes
     # its output symbols only (RAW: all S + 2)
     out_syms = S + 2 if wl.startswith("raw") else S
-    algo = {"k_spec_demod": frames * ((S + 2) * 8 * N * osr + 2 * S), "k_demod_fast": frames * out_syms * (8 * N + 2)}
+    # (round 5: the API and RAW lines run the symbol pass too - API over the data windows only,
+    # RAW over every window with every symbol an output)
+    spec_windows = S if wl.startswith("api") else S + 2
+    algo = {"k_spec_demod": frames * (spec_windows * 8 * N * osr + 2 * out_syms),
+            "k_demod_fast": frames * out_syms * (8 * N + 2)}
     step = 0.0
     d = {"step_kernels": {}}
     for k in sorted(fe):
@@ -113,8 +117,8 @@ for wl, (_, sf, frames, S, _), (pv, pg) in zip(WL, WL.values(), (("pmc1", "pmc5"
                         "valu_busy_frac_4cycle": busy4, "valu_packed_share": PK_SHARE[wl],
                         "valu_instr_per_symbol": vi[k] / (frames * (S + 2))})
     lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | {busy4:.3f} | {busy:.3f} |")
-# round 5: the API / RAW lines' symbol pass (k_demod_fast, scalar fp32: no packed
-# instructions in its body), one SQ_INSTS_VALU + GRBM_GUI_ACTIVE pass each (pmc_valu<tag>)
+# round 5: the API / RAW lines' symbol pass (k_spec_demod since they run the pipeline: the
+# SF7 pass's packed share), one SQ_INSTS_VALU + GRBM_GUI_ACTIVE pass each (pmc_valu<tag>)
 for wl in ("api_sf7", "raw_sf7"):
     tag, sf, frames, S, _ = WL[wl]
     dv = os.path.join(src, f"pmc_valu{tag}")
@@ -127,10 +131,12 @@ for wl in ("api_sf7", "raw_sf7"):
     cyc = gr[k] / XCDS
     busy4 = vi[k] * 4 / (SIMDS * cyc)
     out_syms = S + 2 if wl.startswith("raw") else S
-    summary[wl].update({"valu_instr_per_launch": vi[k], "gpu_cycles_per_launch": cyc, "valu_busy_frac": busy4,
-                        "valu_busy_frac_4cycle": busy4, "valu_packed_share": 0.0,
+    share = PK_SHARE["sf7"] if k.startswith("k_spec_demod") else 0.0
+    busy = busy4 * (share * PK_COST + (1 - share))
+    summary[wl].update({"valu_instr_per_launch": vi[k], "gpu_cycles_per_launch": cyc, "valu_busy_frac": busy,
+                        "valu_busy_frac_4cycle": busy4, "valu_packed_share": share,
                         "valu_instr_per_symbol": vi[k] / (frames * out_syms)})
-    lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | {busy4:.3f} | {busy4:.3f} |")
+    lines.append(f"| {wl} | `{k}` | {vi[k]:.4g} | {cyc:.4g} | {busy4:.3f} | {busy:.3f} |")
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 open(dst, "w").write("\n".join(lines) + "\n")
 json.dump(summary, open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w"), indent=1)
