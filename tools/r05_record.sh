@@ -12,6 +12,13 @@ if [ "$PART" = tests ]; then
   grep -E "pps|dropin_timing|passed|failed|error" $OUT/pytest_gpu.log | tail -25
   exit $rc
 fi
+if [ "$PART" = awgn ]; then
+  # configs[3]: the AWGN sweep SF 7-12, -20 .. +10 dB in 1 dB steps, 0.2-bin CFO, every frame
+  # compared with the exact path and 32 per point with the oracle
+  timeout -k 10 900 python -u tools/awgn_sweep_gpu.py --snr -20 10 1 --cfo 0.2 --out $OUT/awgn_sweep.json > $OUT/awgn_sweep.log 2>&1 || { tail -5 $OUT/awgn_sweep.log; exit 2; }
+  tail -2 $OUT/awgn_sweep.log
+  exit 0
+fi
 if [ "$PART" = prof ]; then
   # bench.py's headline and SF12 lines under the kernel tracer (the same command's HIP-event
   # stage times beside rocprofv3's per-kernel averages), then the two-rank rehearsal on one GPU
