@@ -3,7 +3,9 @@
 // share the load-time runtime's plan and AQL queue (lora_phy_dropin.hip serialises them on the
 // runtime's lock) - and demodulates its own noisy frames (different payloads, delays and
 // amplitudes) `iters` times, every result compared with what the same thread computed alone
-// before the threads started.  Prints one JSON line; tests/test_gpu_dropin.py runs it.
+// before the threads started.  `mixed`: thread t at SF 7 + t (two plans, the one shared
+// queue), each call preceded by a lora_modulate of the thread's packet compared with its
+// first modulation.  Prints one JSON line; tests/test_gpu_dropin.py runs it.
 #include <lora_phy/ChirpGenerator.hpp>
 #include <lora_phy/phy.hpp>
 
@@ -19,7 +21,8 @@
 namespace {
 
 struct Frame {
-  std::vector<std::complex<float>> dech, scratch;
+  std::vector<std::complex<float>> dech, scratch, iq;
+  std::vector<uint16_t> tx;
   std::vector<uint16_t> symbols;
   uint8_t sync = 0;
   float cfo = 0.0f, toff = 0.0f;
@@ -49,6 +52,8 @@ Frame make_frame(unsigned sf, unsigned seed, int delay, float amp, float noise) 
     fr.dech[j] = (iq[src] + std::complex<float>(g(rng), g(rng))) * down[j % N];
   }
   fr.symbols.resize(nsym);
+  fr.iq = iq;
+  fr.tx.assign(symbols.begin(), symbols.begin() + nsym);
   return fr;
 }
 
@@ -67,24 +72,34 @@ bool demod(Frame& fr, unsigned sf, std::vector<uint16_t>& out, uint8_t& sync, fl
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 200;
-  const unsigned sf = 7;
+  const bool mixed = argc > 2 && std::strcmp(argv[2], "mixed") == 0;
   constexpr int kThreads = 2, kFrames = 4;
+  unsigned sfs[kThreads];
   std::vector<Frame> frames[kThreads];
-  for (int t = 0; t < kThreads; ++t)
+  for (int t = 0; t < kThreads; ++t) {
+    sfs[t] = mixed ? 7 + t : 7;
     for (int k = 0; k < kFrames; ++k)
-      frames[t].push_back(make_frame(sf, 100 * t + k, 3 * k + t, 1.0f + 0.5f * k, 0.3f + 0.1f * t));
+      frames[t].push_back(make_frame(sfs[t], 100 * t + k, 3 * k + t, 1.0f + 0.5f * k, 0.3f + 0.1f * t));
+  }
   // each frame alone first (the expected outputs)
   for (int t = 0; t < kThreads; ++t)
     for (Frame& fr : frames[t])
-      if (!demod(fr, sf, fr.symbols, fr.sync, fr.cfo, fr.toff)) return 2;
+      if (!demod(fr, sfs[t], fr.symbols, fr.sync, fr.cfo, fr.toff)) return 2;
   std::atomic<long> calls{0}, bad{0};
   auto work = [&](int t) {
     std::vector<uint16_t> out;
+    std::vector<std::complex<float>> iq;
     for (int i = 0; i < iters; ++i) {
       Frame& fr = frames[t][i % kFrames];
+      if (mixed) {
+        iq.assign(fr.iq.size(), std::complex<float>(0.0f, 0.0f));
+        lora_phy::lora_modulate(fr.tx.data(), fr.tx.size(), iq.data(), sfs[t], 1, lora_phy::bandwidth::bw_125,
+                                1.0f + 0.5f * (float)(i % kFrames), 0x12);
+        if (std::memcmp(iq.data(), fr.iq.data(), iq.size() * sizeof(iq[0])) != 0) ++bad;
+      }
       uint8_t sync = 0;
       float cfo = 0.0f, toff = 0.0f;
-      const bool ok = demod(fr, sf, out, sync, cfo, toff);
+      const bool ok = demod(fr, sfs[t], out, sync, cfo, toff);
       ++calls;
       if (!ok || out != fr.symbols || sync != fr.sync || std::memcmp(&cfo, &fr.cfo, 4) != 0 ||
           std::memcmp(&toff, &fr.toff, 4) != 0)
