@@ -987,6 +987,9 @@ __global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int 
     }
   };
   float phase = 0.0f;
+  // the chain's wave first in the CU's arbitration (its LDS reads queue behind the workers'):
+  // one SF12 frame 1.124 -> 1.090 ms, SF7 unchanged (tools/exp/mod_ab.py --few)
+  if (wk < 0) __builtin_amdgcn_s_setprio(3);
   build(0);
   __syncthreads();
 #ifdef LORA_MF_PROF

@@ -2,7 +2,8 @@
 LORA_MI355X_LIB set), lora_mod_batch of the bench's batches (SF7 and SF12, 15,625 frames x 64
 symbols) into one preallocated output, HIP events around `reps` calls, alternating libraries
 over `rounds` rounds; every variant's output hashed against the first library's.
-usage: python tools/exp/mod_ab.py [--rounds R] [--reps K] base mph4 ..."""
+--few: k_mod_frame's shapes instead (1 and 64 frames at SF7, 1 at SF12).
+usage: python tools/exp/mod_ab.py [--rounds R] [--reps K] [--few] base mph4 ..."""
 import argparse
 import json
 import os
@@ -19,7 +20,7 @@ sys.path.insert(0, PKG)
 import lora_phy_amd as amd
 reps = REPS
 res = {}
-for sf, frames in ((7, 15625), (12, 15625)):
+for sf, frames in WORKS:
     g = torch.Generator(device="cpu").manual_seed(sf)
     syms = torch.randint(0, 1 << sf, (frames, 64), generator=g, dtype=torch.int32).to(torch.uint16).cuda()
     out = amd.modulate(syms, sf)
@@ -30,8 +31,8 @@ for sf, frames in ((7, 15625), (12, 15625)):
         amd.modulate(syms, sf, out=out)
     e1.record()
     torch.cuda.synchronize()
-    h = hashlib.sha256(out[::97].cpu().numpy().tobytes()).hexdigest()[:16]
-    res[f"sf{sf}"] = {"ms": e0.elapsed_time(e1) / reps, "hash": h}
+    h = hashlib.sha256(out.reshape(-1)[::97].cpu().numpy().tobytes()).hexdigest()[:16]
+    res[f"sf{sf}x{frames}"] = {"ms": e0.elapsed_time(e1) / reps, "hash": h}
     del out
     torch.cuda.empty_cache()
 print(json.dumps(res))
@@ -43,8 +44,10 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--few", action="store_true", help="k_mod_frame's shapes: 1 and 64 frames")
     args = ap.parse_args()
-    code = CHILD.replace("PKG", repr(PKG)).replace("REPS", str(args.reps))
+    works = "((7, 1), (7, 64), (12, 1))" if args.few else "((7, 15625), (12, 15625))"
+    code = CHILD.replace("PKG", repr(PKG)).replace("REPS", str(args.reps)).replace("WORKS", works)
     rows = {n: [] for n in args.libs}
     for r in range(args.rounds):
         for name in args.libs:
@@ -60,8 +63,7 @@ def main():
     ref = rows[args.libs[0]][0]
     for name, rs in rows.items():
         same = all(x[k]["hash"] == ref[k]["hash"] for x in rs for k in ref)
-        print(json.dumps({"lib": name, "sf7_ms": [round(x["sf7"]["ms"], 4) for x in rs],
-                          "sf12_ms": [round(x["sf12"]["ms"], 3) for x in rs], "same_output": same}))
+        print(json.dumps({"lib": name, **{k: [round(x[k]["ms"], 4) for x in rs] for k in ref}, "same_output": same}))
 
 
 if __name__ == "__main__":
