@@ -194,6 +194,12 @@ int lora_demod_last_kernels(const lora_demod_plan* plan);
  * pipeline (three launches: frame max, estimate, demod). */
 int64_t lora_demod_spec_recomputed(lora_demod_plan* plan);
 
+/* Choose the plan's path explicitly (instead of the process-wide LORA_MI355X_SPEC read at
+ * plan creation): speculative = 1 runs the speculative single-read pipeline wherever it
+ * covers the configuration (the default), 0 always the three-launch exact path.  Both give
+ * the reference's outputs; the second is the pipeline's checker in the tests.  Returns 0. */
+int lora_demod_plan_set_pipeline(lora_demod_plan* plan, int speculative);
+
 /* Diagnostics of the C++ drop-in's private AQL queue (liblora_phy.so): with
  * LORA_MI355X_AQL_PROFILE=1 set before the queue is created, every dispatch is timestamped
  * and this returns the last call's timeline in microseconds relative to its doorbell:

@@ -790,7 +790,7 @@ __global__ void __launch_bounds__(kMfThreads) k_mod_frame(ModArgs a, int W, int 
     const unsigned v = chirp_value(a, fr, c);
     if (a.seg && (int)v < a.seg_n) {
       // the precomputed runs of this chirp value (mod_run_table): a copy, 16 bytes per load
-      const int nr = a.cnt[v];
+      const int nr = min(a.cnt[v], kMfSegMax);  // (< 0: the runs overflowed, the recurrence below)
       tcnt[slot][j] = nr;
       const uint4* src = reinterpret_cast<const uint4*>(a.seg + (size_t)v * a.seg_cap);
       uint4* dst = reinterpret_cast<uint4*>(tab[slot][j]);
@@ -1279,6 +1279,12 @@ int lora_demod_plan_create(const lora_demod_params* params, lora_demod_plan** ou
   return LORA_OK;
 }
 
+int lora_demod_plan_set_pipeline(lora_demod_plan* plan, int speculative) {
+  if (!plan || (speculative != 0 && speculative != 1)) return set_error(LORA_EINVAL, "bad argument");
+  plan->spec = speculative;
+  return LORA_OK;
+}
+
 int lora_demod_profile_enable(lora_demod_plan* plan, int max_calls) {
   if (!plan || max_calls < 0) return set_error(LORA_EINVAL, "bad argument");
   int prev = 0;
@@ -1592,10 +1598,13 @@ bool mod_run_table(ModArgs& a, int sf, hipStream_t st) {
     if (t.seg) hipFree(t.seg);
     return set_error(LORA_EIO, "hipMalloc"), false;
   }
-  // (recorded with the frame kernel when the C++ drop-in dispatches on its AQL queue: the
-  // packets run in order; otherwise built and waited for here, once)
-  lora::launch(k_mod_runs, dim3((unsigned)((t.n + 63) / 64)), dim3(64), 0, st, a, t.n, t.cap, t.seg, t.cnt);
-  if (!lora::t_launch_record && hipStreamSynchronize(st) != hipSuccess) {
+  // Built and waited for here, once, always through HIP - also while the C++ drop-in records
+  // launches for its AQL queue (then on the null stream): an entry enters g_mrt only once its
+  // tables are complete, so no caller (another thread's lora_mod_batch, or this one after the
+  // queue refused its record) can find a table that was never filled.
+  hipStream_t bst = lora::t_launch_record ? nullptr : st;
+  hipLaunchKernelGGL(k_mod_runs, dim3((unsigned)((t.n + 63) / 64)), dim3(64), 0, bst, a, t.n, t.cap, t.seg, t.cnt);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(bst) != hipSuccess) {
     hipFree(t.seg);
     hipFree(t.cnt);
     return set_error(LORA_EIO, "k_mod_runs"), false;
@@ -1652,14 +1661,19 @@ int64_t lora_mod_batch(unsigned sf, unsigned osr, unsigned bw_hz, float amplitud
   a.seg = nullptr;
   a.cnt = nullptr;
   a.seg_n = a.seg_cap = 0;
-  if (frames <= kMfMaxFrames) {
+  // k_mod_frame's windows hold whole chirps or an exact fraction of one (a window never
+  // crosses a chirp boundary inside it), and with chirps of whole 32-sample blocks whole
+  // blocks: osr values that break either (SF10 osr 5: 5,120-sample chirps, 1,706-sample
+  // windows) take the bulk kernels
+  const int W = step <= kMfWin ? step * (kMfWin / step) : step / ((step + kMfWin - 1) / kMfWin);
+  const bool mf_ok = (step <= W ? W % step == 0 : step % W == 0) && (step % kMfBlk != 0 || W % kMfBlk == 0);
+  if (frames <= kMfMaxFrames && mf_ok) {
     // few frames: a workgroup per frame, windows of whole chirps or exact chirp fractions;
     // long chirps from the configuration's run tables (built here on first use)
     if (step >= kMfTabMin && !mod_run_table(a, (int)sf, st)) {
       if (prev != device) hipSetDevice(prev);
       return set_error(LORA_EIO, "modulator run tables: " + g_last_error);
     }
-    const int W = step <= kMfWin ? step * (kMfWin / step) : step / ((step + kMfWin - 1) / kMfWin);
     const int64_t nwin = (per_frame + W - 1) / W;
     lora::launch(k_mod_frame, dim3((unsigned)frames), dim3(kMfThreads), 0, st, a, W, (int)nwin);
   } else {

@@ -73,8 +73,9 @@ uint16_t sx1272_data_checksum(const uint8_t* data, int length) {
 
 size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
-// lora_phy_dropin_last_timing: the last AQL demodulation's and modulation's phases (us)
-double g_timing[8] = {};
+// lora_phy_dropin_last_timing: the calling thread's last AQL demodulation's and modulation's
+// phases (us); per thread, so concurrent drop-in calls neither race on it nor mix their values
+thread_local double g_timing[8] = {};
 
 double now_us() {
   timespec t;
@@ -337,9 +338,15 @@ bool run_frame(lora_phy::detail::device_state& g, const std::complex<float>* sam
   o.cfo = reinterpret_cast<float*>(dev + d.cfo);
   o.time_offset = reinterpret_cast<float*>(dev + d.toff);
   o.max_amp = reinterpret_cast<float*>(dev + d.maxa);
-  if (lora_demod_batch(g.plan, reinterpret_cast<const float*>(dev + d.iq), 1, (int64_t)count, (int64_t)count, &o,
-                       dev + d.ws, d.total - d.ws, st) < 0)
-    return false;
+  {
+    // a shared plan's bookkeeping (last_kernels, the recompute counter) is written by
+    // lora_demod_batch: the runtime's lock, as on the queue path
+    std::unique_lock<std::mutex> lk(rt().mu, std::defer_lock);
+    if (g.shared_plan) lk.lock();
+    if (lora_demod_batch(g.plan, reinterpret_cast<const float*>(dev + d.iq), 1, (int64_t)count, (int64_t)count, &o,
+                         dev + d.ws, d.total - d.ws, st) < 0)
+      return false;
+  }
   // symbols, then the four per-frame outputs (256-byte slots, contiguous): two copies
   if ((nsym > 0 && hipMemcpyAsync(host + d.syms, dev + d.syms, (size_t)nsym * sizeof(uint16_t),
                                   hipMemcpyDeviceToHost, st) != hipSuccess) ||

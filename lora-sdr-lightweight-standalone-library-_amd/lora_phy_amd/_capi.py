@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "lora_demod_profile_read",
     "lora_demod_last_kernels",
     "lora_demod_spec_recomputed",
+    "lora_demod_plan_set_pipeline",
     "lora_aql_last_profile",
     "lora_last_error",
     "lora_version",
@@ -122,6 +123,8 @@ def lib() -> C.CDLL:
     L.lora_demod_last_kernels.argtypes = [C.c_void_p]
     L.lora_demod_spec_recomputed.restype = C.c_int64
     L.lora_demod_spec_recomputed.argtypes = [C.c_void_p]
+    L.lora_demod_plan_set_pipeline.restype = C.c_int
+    L.lora_demod_plan_set_pipeline.argtypes = [C.c_void_p, C.c_int]
     L.lora_aql_last_profile.restype = C.c_int
     L.lora_aql_last_profile.argtypes = [C.POINTER(C.c_double), C.c_int]
     L.lora_last_error.restype = C.c_char_p

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes as C
-import os
+import threading
 from dataclasses import dataclass
 from typing import Optional
 
@@ -76,7 +76,12 @@ class DemodPlan:
     """A device plan for one demodulator configuration (lora_demod_init equivalent)."""
 
     def __init__(self, sf: int, osr: int = 1, bw: int = 125000, window="none",
-                 dechirp: bool = False, mode: str = "legacy", device=None, precision: str = "exact"):
+                 dechirp: bool = False, mode: str = "legacy", device=None, precision: str = "exact",
+                 pipeline: Optional[str] = None):
+        """``pipeline``: "spec" = the speculative single-read pipeline wherever it covers the
+        configuration, "split" = always the three-launch exact path; None = the enclosing
+        ``spec_pipeline`` block's choice on this thread, else the library default (spec,
+        unless LORA_MI355X_SPEC=0 was set when the plan was created)."""
         if not torch.cuda.is_available():
             raise RuntimeError("lora_phy_amd needs a HIP GPU (torch.cuda.is_available() is False)")
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else
@@ -97,6 +102,13 @@ class DemodPlan:
         h = C.c_void_p()
         _capi.check(self._lib.lora_demod_plan_create(C.byref(prm), C.byref(h)))
         self._h = h
+        if pipeline is None:
+            pipeline = getattr(_PIPELINE, "choice", None)
+        if pipeline is not None:
+            if pipeline not in ("spec", "split"):
+                raise ValueError('pipeline must be "spec", "split" or None')
+            _capi.check(self._lib.lora_demod_plan_set_pipeline(h, int(pipeline == "spec")))
+        self.pipeline = pipeline
         # Workspaces per stream (two streams never share frame maxima / FrameParams);
         # ones used while a HIP graph was being captured are kept for the plan's lifetime,
         # since the graph replays with their addresses.
@@ -254,19 +266,19 @@ class LoRaDemod:
         return self.last.sync == self.sync
 
 
+_PIPELINE = threading.local()
+
+
 @contextlib.contextmanager
 def spec_pipeline(enabled: bool = True):
-    """Plans created inside this block use the speculative single-read pipeline (the
-    default) or, with ``enabled=False``, the three-launch exact path (frame max, estimate,
-    demod: ``LORA_MI355X_SPEC=0``, read by lora_demod_plan_create).  The caller's own value
-    of the variable is restored on exit, not removed."""
-    prev = os.environ.get("LORA_MI355X_SPEC")
-    if not enabled:
-        os.environ["LORA_MI355X_SPEC"] = "0"
+    """Plans created inside this block ON THIS THREAD use the speculative single-read pipeline
+    (``enabled=True``, whatever LORA_MI355X_SPEC says) or the three-launch exact path (frame
+    max, estimate, demod: ``enabled=False``) - ``DemodPlan(pipeline=...)`` with the choice
+    filled in.  Nothing process-wide changes (no environment variable is touched), so other
+    threads creating plans meanwhile are unaffected; blocks nest."""
+    prev = getattr(_PIPELINE, "choice", None)
+    _PIPELINE.choice = "spec" if enabled else "split"
     try:
         yield
     finally:
-        if prev is None:
-            os.environ.pop("LORA_MI355X_SPEC", None)
-        else:
-            os.environ["LORA_MI355X_SPEC"] = prev
+        _PIPELINE.choice = prev

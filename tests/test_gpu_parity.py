@@ -178,14 +178,17 @@ def test_modulator_many_frames_matches_oracle(O, amd, sf, frames):
 @pytest.mark.parametrize("sf,osr,S,frames,big", [(7, 1, 64, 1, False), (7, 1, 64, 1, True), (8, 3, 40, 3, True),
                                                   (10, 1, 30, 2, True), (11, 3, 6, 2, False), (12, 1, 10, 1, True),
                                                   (12, 4, 3, 2, False), (2, 1, 50, 4, True), (9, 2, 20, 512, False),
-                                                  (9, 2, 20, 513, False)])
+                                                  (9, 2, 20, 513, False), (10, 5, 6, 3, False), (10, 9, 4, 2, True),
+                                                  (9, 5, 8, 2, False), (12, 3, 3, 1, False)])
 def test_modulator_frame_kernel_matches_oracle(O, amd, sf, osr, S, frames, big):
     """Up to 512 frames take k_mod_frame (a workgroup per frame: frequencies from the runs of
     csrc/lora_chirp.h or the per-chirp recurrence, one lane's phase chain, parallel sincosf)
     - 513 the bulk kernels.  Windows of whole chirps and of chirp fractions (osr 3/4 at
     SF 11/12), partial last windows, and symbols >= N (lora_encode's codewords reach 255;
     `big`: uint16 values up to 65535, whose chirps may overflow the run table and fall back
-    to the recurrence) - every sample bit for bit against the oracle."""
+    to the recurrence) - every sample bit for bit against the oracle.  osr 5 at SF10 (5,120-sample
+    chirps) and osr 9 have no window length that is an exact fraction of a chirp: they take the
+    bulk kernels - checked the same way."""
     rng = np.random.default_rng(sf * 131 + osr + frames)
     hi = 65536 if big else (1 << sf)
     syms = rng.integers(0, hi, (frames, S)).astype(np.uint16)
