@@ -180,6 +180,13 @@ def make_input(sf, frames, data_syms, seed, device, snr_db=None, sync=None, osr=
 
 
 LAUNCH = "eager"  # --launch: "eager" (plan.run per step, default) or "graph" (HIP graph replay of the step)
+# --prewarm-ms: untimed steps of the same workload, for at least this long, before the W warmup
+# steps - so that the K timed steps see the GPU's sustained state even when K and W are small.
+# (Round 6, one box, headline only: 20 timed steps after 5 warmup steps measured 0.2627 and
+# 0.2701 ms per step, 100 after 10 0.2521: a few ms of work after a cold start runs below the
+# sustained rate.)
+PREWARM_MS_DEFAULT = 300.0
+PREWARM_MS = PREWARM_MS_DEFAULT
 
 
 def stage_times(plan, iq, out, steps, device):
@@ -222,6 +229,11 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
         plan = amd.DemodPlan(sf, osr, 125000, window, dechirp=True, mode=mode, device=device,
                              precision=precision)
     out = None
+    t_warm = time.perf_counter()
+    while (time.perf_counter() - t_warm) * 1e3 < PREWARM_MS:  # untimed pre-warm (PREWARM_MS)
+        for _ in range(8):
+            out = plan.run(iq, out)
+        torch.cuda.synchronize(device)
     for _ in range(warmup):
         out = plan.run(iq, out)
     torch.cuda.synchronize(device)
@@ -723,9 +735,13 @@ def main():
     ap.add_argument("--plumbing", action="store_true",
                     help="form the ranks and report them without touching a GPU (CPU test of the "
                          "multi-rank launch)")
+    ap.add_argument("--prewarm-ms", type=float, default=PREWARM_MS_DEFAULT,
+                    help="untimed steps of each workload for at least this long before its W warmup steps "
+                         "(0: none)")
     args = ap.parse_args()
-    global LAUNCH
+    global LAUNCH, PREWARM_MS
     LAUNCH = args.launch
+    PREWARM_MS = args.prewarm_ms
     global SYNC
     SYNC = args.sync
 
@@ -917,7 +933,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (GPU lora_modulate of seeded random symbols, amplitude 1, no noise)",
-            "config": {"workload": workload, "launch": LAUNCH, "sf": 7, "bw_hz": 125000, "osr": 1,
+            "config": {"workload": workload, "launch": LAUNCH, "prewarm_ms": PREWARM_MS, "sf": 7, "bw_hz": 125000,
+                       "osr": 1,
                        "frames_per_gpu": args.frames, "data_symbols_per_frame": args.data_symbols,
                        "parallelism": f"frames sharded x{world}, no collective (gloo timing only)",
                        "ranks": ranks, "symbols_ok": r7["symbols_ok"], "parity": r7["parity"],

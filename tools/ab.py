@@ -1,6 +1,6 @@
-"""Same-box A/B of library builds on chosen workloads (round 5 development).
+"""Same-box A/B of library builds on chosen workloads (any round).
 
-usage: python tools/r05_ab.py [--reps 3] [--steps 100] [--work sf7,awgn0,awgn10,...] name [name ...]
+usage: python tools/ab.py [--reps 3] [--steps 100] [--work sf7,awgn0,awgn10,...] name [name ...]
   name "default" = the in-tree library; any other name = lora_phy_amd/lib/variants/<name>.so
   (tools/build_variant.sh).  Each (rep, variant) runs in its own process, interleaved;
   prints one line per run: variant, then per workload ms_per_step and the symbol-pass ms.
