@@ -930,6 +930,12 @@ constexpr size_t spec_lds_bytes() {
              : sizeof(cf) * ((size_t)Geo<SF>::SPW * lds_row<SF>() + demod_twl_entries<SF, true>());
 }
 
+// osr 4 in the symbol pass: whole-line loads with a lane move (1) or two half-line loads per
+// point (0, rounds 4-5)
+#ifndef LORA_OSR4_LINES
+#define LORA_OSR4_LINES 1
+#endif
+
 // SPEC: the speculative single-read pipeline's symbol pass (lora_capi.hip): the pre-pass
 // offsets (fp_spec) on unscaled samples, and per data symbol (spec_marg, one 8-byte
 // store) the margin |X1| - |X2| between the top bin and the runner-up and the window's
@@ -1150,7 +1156,42 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       const int vo = rel + (int)(base + (int64_t)l * osr) * 8;
       const int vt = (cg + l * osr) * 8;
       const int so = T * osr * 8;  // bytes between a lane's points
-      if constexpr (OSRV == 2 || OSRV == 4) {
+      if constexpr (OSRV == 4 && LORA_OSR4_LINES) {
+        // osr 4, whole lines: load i (< 2P) covers 2T consecutive samples of the window, lane l
+        // the pair base + 2T i + 2l, +1 (16 bytes; a wave instruction reads whole 128-byte
+        // lines).  The points (every 4th sample) are the first of an even lane's pairs - those
+        // of even i role l/2's points, those of odd i role T/2 + l/2's, which the odd lane
+        // l + 1 takes by a row_shr:1 lane move: every byte read once, by one load, in whole
+        // lines (the two half-line 16-byte loads per point fetched 1.24x the window's bytes).
+        const bool odd = (l & 1) != 0;
+        lr = odd ? T / 2 + (l >> 1) : (l >> 1);
+        const int vo2 = rel + (int)base * 8 + 16 * l;
+        const int vt2 = (cg + 2 * l) * 8;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          cf e0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * q + h;
+            const float4 y2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo2, i * 2 * T * 8, 2 /* nt */));
+            cf y0 = cf{y2.x, y2.y}, y1 = cf{y2.z, y2.w};
+            if constexpr (MODE == 0) {
+              const float4 d2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, vt2, i * 2 * T * 8, 0));
+              y0 = pk_cmul_ref(y0, cf{d2.x, d2.y});
+              y1 = pk_cmul_ref(y1, cf{d2.z, d2.w});
+            }
+            if constexpr (!SYNC) pm = amax3(amax3(pm, y0), y1);
+            if (h == 0) {
+              e0 = y0;
+            } else {
+              // lane l - 1's pair (row_shr:1; even lanes' own values are replaced below)
+              const cf m = cf{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y0.re), 0x111, 0xF, 0xF, false)),
+                              __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y0.im), 0x111, 0xF, 0xF, false))};
+              in[q] = odd ? m : e0;
+            }
+          }
+        }
+      } else if constexpr (OSRV == 2 || OSRV == 4) {
         // the point's osr consecutive samples (and table values) two per 16-byte load: every
         // byte of the window is fetched by exactly one load (8-byte loads of every osr-th
         // sample, osr of them over the same lines, cost 1.31x the window's bytes at osr 2
