@@ -7,7 +7,7 @@ CFO rotation, FFT, argmax, sync word.  Inputs are generated on the device by the
 bit-exact GPU modulator (lora_mod_batch), random symbols from a fixed seed.  Each step is
 one plan.run (the pipeline's four kernels enqueued on the stream; `--launch graph` replays
 them as a captured HIP graph instead, whose per-replay cost made it 2 % slower at SF7 in
-round 5's same-box A/B, tools/r05_launch_ab.sh).
+round 5's same-box A/B).
 
 Headline workload (BASELINE.json configs[1]): SF7 BW125 osr 1, 1,000,000 data symbols
 = 15,625 frames x (2 sync + 64 data) per GPU.  The SF12 configuration (configs[2]) and
@@ -691,7 +691,7 @@ def roofline(r, probe=None):
             "bytes_per_launch": r["dominant_bytes_per_launch"],
             "traffic": pmc_dom,
             "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch, "
-                              "tools/pmc_r04.py; committed, not measured in this run)",
+                              "tools/pmc_traffic.py; committed, not measured in this run)",
             # the kernel's other roof: VALU issue (SQ_INSTS_VALU x its issue cycles - 4 per
             # instruction, packed ones weighted by their 0.58 issue rate - over 1024 SIMDs x the
             # GRBM-measured cycles of the same launch, committed profile)
@@ -699,7 +699,7 @@ def roofline(r, probe=None):
                      "busy_frac_4cycle": load_pmc(wl, "valu_busy_frac_4cycle"),
                      "instr_per_symbol": load_pmc(wl, "valu_instr_per_symbol"),
                      "source": "profiles/pmc_summary.json (rocprofv3 SQ_INSTS_VALU, GRBM_GUI_ACTIVE; "
-                               "tools/pmc_r04.py)"},
+                               "tools/pmc_traffic.py)"},
             "pipeline": {"algorithmic_bytes_per_step": r["step_bytes"], "ms_per_step": r["ms_per_step"],
                          "achieved": r["pipeline_gbs"], "pipeline_frac": r["pipeline_gbs"] / HBM_PEAK_GBS,
                          "counter_bytes_per_step": pmc_step,
@@ -715,7 +715,7 @@ def main():
                     help="step launch: plan.run per step (default: the step's four kernels enqueued on the "
                          "stream, about 1.5-2 us between dependent kernels), or one HIP-graph replay of the "
                          "step's launches (the same kernels on the same buffers, captured once; each replay "
-                         "adds about 9.5 us before the next step - round 5: 2 % slower, tools/r05_launch_ab.sh)")
+                         "adds about 9.5 us before the next step - round 5: 2 % slower)")
     # 100 timed steps (33 ms at SF7): with 20 (6 ms) a single host or clock hiccup moved the
     # per-step time by several percent between runs of the same build
     ap.add_argument("--steps", type=int, default=100)

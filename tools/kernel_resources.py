@@ -1,6 +1,6 @@
 """Per-kernel resources from the code-object metadata of the built library (not the trace):
 VGPRs, AGPRs, SGPRs, scratch bytes per lane (private segment), static LDS, and the dynamic
-LDS the launch adds where the host code sets one (tools/prof_r04.py joins this with rocprofv3
+LDS the launch adds where the host code sets one (tools/kernel_stats.py joins this with rocprofv3
 kernel statistics).  usage: python tools/kernel_resources.py [lib.so] [name-regex] [--json]
 """
 import json

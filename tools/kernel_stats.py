@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise a round-4 profiling call (tools/r04_prof.sh output) into markdown: per-kernel
+"""Summarise a profiling call (PART=trace / pmc bash tools/record.sh -> gpurun_out/rec/prof) into
+markdown (profiles/rNN/kernel_stats.md): per-kernel
 rocprofv3 kernel-trace statistics of each bench workload run alone (kt7: SF7 headline,
 kt7n10: SF7 at -10 dB, kt12: SF12, kt7o2: SF7 osr 2 - each run launches only that
 workload's pipeline), with each kernel's resources taken from the code-object metadata of
@@ -7,7 +8,7 @@ the built library (tools/kernel_resources.py: VGPRs, scratch bytes per lane, sta
 not from the trace; then SQ counters per launch of the pipeline kernels (pmcN passes, one
 rocprofv3 --pmc run each).
 
-usage: prof_r04.py <gpurun_out/dir> [out.md]"""
+usage: [PROF_ROUND=6] kernel_stats.py gpurun_out/rec/prof profiles/r06/kernel_stats.md"""
 import collections
 import csv
 import glob
@@ -27,7 +28,7 @@ TAGS = {"kt7": "SF7 headline (15,625 frames x 66 symbols, noiseless)",
         "kt7o4": "SF7 osr 4 (15,625 frames x 66 symbols, noiseless)",
         "kt7api": "SF7 API mode (phy::demodulate, same shape)",
         "kt7raw": "SF7 RAW mode (detector per symbol, same shape)"}
-ROUND = os.environ.get("PROF_ROUND", "4")
+ROUND = os.environ.get("PROF_ROUND", "6")
 
 
 def short(name):

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """HBM traffic per kernel launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-(tools/r04_prof.sh: <dir>/pmc_fetch<tag>, <dir>/pmc_write<tag>), with the gfx950 correction
+(PART=pmc bash tools/record.sh: <dir>/pmc_fetch<tag>, <dir>/pmc_write<tag>), with the gfx950 correction
 from MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of a wide coalesced read:
 doubled).  Writes <out>.md and profiles/pmc_summary.json (read by bench.py for
 roofline.traffic): per workload the dominant kernel's HBM bytes per launch and the step's.
 
-usage: [PROF_ROUND=5] pmc_r04.py <gpurun_out/prof4> <profiles/r04/pmc_traffic.md>"""
+usage: [PROF_ROUND=6] pmc_traffic.py gpurun_out/rec/prof profiles/r06/pmc_traffic.md"""
 import collections
 import csv
 import glob
@@ -36,10 +36,10 @@ def per_kernel(d, counter):
 # algorithmic bytes per launch of the dominant kernel: data symbols x (8N + 2)
 # workload: (tag of the pmc_* dirs, sf, frames, data symbols, osr)
 WL = {"sf7": ("7", 7, 15625, 64, 1), "sf12": ("12", 12, 4000, 64, 1), "osr2_sf7": ("7o2", 7, 15625, 64, 2),
-      # round 5 (tools/r05_prof.sh): osr 4, and bench.py's API / RAW receiver lines, whose
+      # (round 5 on) osr 4, and bench.py's API / RAW receiver lines, whose
       # symbol pass is k_demod_fast (RAW: every symbol an output)
       "osr4_sf7": ("7o4", 7, 15625, 64, 4), "api_sf7": ("7api", 7, 15625, 64, 1), "raw_sf7": ("7raw", 7, 15625, 64, 1)}
-ROUND = os.environ.get("PROF_ROUND", "4")
+ROUND = os.environ.get("PROF_ROUND", "6")
 summary, lines = {}, [f"# HBM traffic per launch, rocprofv3 FETCH_SIZE / WRITE_SIZE (r0{ROUND})", "",
                       "FETCH_SIZE / WRITE_SIZE in KB as reported; `read B (x2)` applies the gfx950 correction "
                       "(MI355X_MICROARCH.md: FETCH_SIZE = half the bytes of a coalesced read).  Workloads: "
@@ -88,7 +88,7 @@ for wl, (tag, sf, frames, S, osr) in WL.items():
             d[key] = d[key] * scale
     summary[wl] = d
     lines.append(f"| {wl} | whole step | | | | {step:.4g} | {step_algo:.4g} | {step / step_algo:.4f} |")
-# VALU issue of the symbol pass from the SQ passes (tools/r04_prof.sh: pmc1/pmc2 hold
+# VALU issue of the symbol pass from the SQ passes (PART=pmc: pmc1/pmc2 hold
 # SQ_INSTS_VALU, pmc5/pmc6 GRBM_GUI_ACTIVE for sf7/sf12): counted as 4 cycles per wave64 VALU
 # instruction (a packed fp32 instruction issues at ~0.58 of the scalar rate,
 # tools/micro/valu_rate.hip, so this under-counts a packed-heavy body); GRBM_GUI_ACTIVE sums

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A pipeline step's timeline from a rocprofv3 kernel trace (tools/r05_prof.sh's bench7 /
+"""A pipeline step's timeline from a rocprofv3 kernel trace (PART=trace bash tools/record.sh: gpurun_out/rec/prof/bench7 /
 kt7 directories): for every run of consecutive pipeline kernels that starts with the
 pre-pass, each kernel's duration and the gap before it, then the medians over the steps.
 usage: step_timeline.py <trace dir> [first kernel prefix (default k_est)]"""
