@@ -187,6 +187,14 @@ LAUNCH = "eager"  # --launch: "eager" (plan.run per step, default) or "graph" (H
 # sustained rate.)
 PREWARM_MS_DEFAULT = 300.0
 PREWARM_MS = PREWARM_MS_DEFAULT
+# --streams: consecutive steps (batches) go round-robin to this many HIP streams, each with
+# its own workspace (DemodPlan keeps one per stream) and outputs - a receiver with that many
+# batches in flight, so one batch's latency-bound estimate stages run beside the next one's
+# kernels.  Every step still runs the whole pipeline on its whole batch inside the timed
+# region.  (Round 6, one box, tools/streams_probe.py: SF7 0.2376-0.2406 ms per step on one
+# stream, 0.2205-0.2259 on two, 0.2203-0.2211 on three; SF12 4,000 frames -4 % on two.)
+STREAMS_DEFAULT = 2
+STREAMS = STREAMS_DEFAULT
 
 
 def stage_times(plan, iq, out, steps, device):
@@ -212,7 +220,7 @@ def stage_times(plan, iq, out, steps, device):
 
 def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, precision="exact",
                inputs=None, sync=None, seed_base=20251015, rank=0, window="none", osr=1, spec=True,
-               mode="legacy"):
+               mode="legacy", streams=None):
     """mode "legacy": lora_demodulate with the fused caller dechirp (the headline); "api":
     lora_phy::demodulate (phy.cpp:178-239: estimate on the raw samples, down-chirp fused per
     symbol); "raw": the detector alone per symbol (dechirp -> FFT -> argmax, the AWGN
@@ -229,14 +237,26 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
         plan = amd.DemodPlan(sf, osr, 125000, window, dechirp=True, mode=mode, device=device,
                              precision=precision)
     out = None
+    # the steps' streams (STREAMS; one for a graph replay): step k on stream k mod S, with
+    # outputs of its own
+    S = 1 if LAUNCH == "graph" else max(1, STREAMS if streams is None else streams)
+    main_stream = torch.cuda.current_stream(device)
+    sts = [main_stream] if S == 1 else [torch.cuda.Stream(device) for _ in range(S)]
+    outs = [None] * S
+
+    def run_step(k):
+        with torch.cuda.stream(sts[k % S]):
+            outs[k % S] = plan.run(iq, outs[k % S])
+
     t_warm = time.perf_counter()
     while (time.perf_counter() - t_warm) * 1e3 < PREWARM_MS:  # untimed pre-warm (PREWARM_MS)
-        for _ in range(8):
-            out = plan.run(iq, out)
+        for k in range(8):
+            run_step(k)
         torch.cuda.synchronize(device)
-    for _ in range(warmup):
-        out = plan.run(iq, out)
+    for k in range(max(warmup, S)):
+        run_step(k)
     torch.cuda.synchronize(device)
+    out = outs[0]
     step = None
     if LAUNCH == "graph":
         # the step's launches captured once into a HIP graph and replayed (the same kernels
@@ -256,14 +276,27 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     barrier(dist)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for st in sts:
+        if st is not main_stream:
+            st.wait_stream(main_stream)
+    for k in range(steps):
         if step is not None:
             step()
         else:
-            out = plan.run(iq, out)
+            run_step(k)
+    for st in sts:
+        if st is not main_stream:
+            main_stream.wait_stream(st)
     torch.cuda.synchronize(device)
     barrier(dist)
     wall = time.perf_counter() - t0
+    if step is None:
+        out = outs[0]
+        # every stream's outputs are the same batch's: equal to stream 0's, symbol for symbol
+        streams_equal = all(bool(torch.equal(o.symbols, out.symbols)) and bool(torch.equal(o.sync, out.sync))
+                            for o in outs)
+    else:
+        streams_equal = True
     fixed = (plan.spec_recomputed() - fixed0) / steps
     kernels = sorted(plan.last_kernels())
     stage_ms, out = stage_times(plan, iq, out, steps, device)
@@ -281,6 +314,8 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
         ser = float((got != torch.cat([head.expand(frames, 2), syms], 1)).float().mean())
     else:
         ser = float((got != syms).float().mean())
+    if not streams_equal:
+        ser = max(ser, 1.0)  # a stream's outputs differ from stream 0's: not ok
     # the symbol pass in the speculative pipeline (ranks sharing a device in a rehearsal
     # can distort the stage times); otherwise the longest stage
     dom = 2 if "spec" in kernels else max(range(3), key=lambda k: stage_ms[k])
@@ -305,6 +340,7 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
         "sf": sf, "osr": osr, "mode": mode, "window": window, "precision": precision,
         "frames": frames, "data_symbols": frames * out_syms, "iq_bytes": iq.numel() * 8,
         "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ser == 0.0, "ser_vs_tx": ser,
+        "streams": S,
         "kernels": kernels, "spec_recomputed_per_step": fixed,
         "msym_s_data": frames * out_syms / (ms_step * 1e-3) / 1e6,
         "msym_s_all_ranks": units / wall_max / 1e6, "ms_per_step_max_rank": wall_max * 1e3 / steps,
@@ -735,13 +771,17 @@ def main():
     ap.add_argument("--plumbing", action="store_true",
                     help="form the ranks and report them without touching a GPU (CPU test of the "
                          "multi-rank launch)")
+    ap.add_argument("--streams", type=int, default=STREAMS_DEFAULT,
+                    help="HIP streams the consecutive steps go to, round-robin (each its own workspace and "
+                         "outputs: that many batches in flight); 1 = every step on one stream")
     ap.add_argument("--prewarm-ms", type=float, default=PREWARM_MS_DEFAULT,
                     help="untimed steps of each workload for at least this long before its W warmup steps "
                          "(0: none)")
     args = ap.parse_args()
-    global LAUNCH, PREWARM_MS
+    global LAUNCH, PREWARM_MS, STREAMS
     LAUNCH = args.launch
     PREWARM_MS = args.prewarm_ms
+    STREAMS = args.streams
     global SYNC
     SYNC = args.sync
 
@@ -768,6 +808,14 @@ def main():
         return
     r7 = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank)
     r7["parity"] = exact_parity(r7, device)
+    one = None
+    if r7["streams"] > 1:
+        # the same workload with every step on one stream (batches back to back)
+        r1 = run_config(7, args.frames, args.data_symbols, args.steps, args.warmup, dist, device, rank=rank,
+                        inputs=(r7["syms"], r7["iq"]), streams=1)
+        one = {"ms_per_step": r1["ms_per_step_max_rank"], "value_all_ranks_msym_s": r1["msym_s_all_ranks"],
+               "symbols_ok": r1["symbols_ok"]}
+        del r1
     probe = None
     try:
         probe = hbm_probe(device)
@@ -933,7 +981,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (GPU lora_modulate of seeded random symbols, amplitude 1, no noise)",
-            "config": {"workload": workload, "launch": LAUNCH, "prewarm_ms": PREWARM_MS, "sf": 7, "bw_hz": 125000,
+            "config": {"workload": workload, "launch": LAUNCH, "prewarm_ms": PREWARM_MS,
+                       "streams": r7["streams"], "one_stream": one, "sf": 7, "bw_hz": 125000,
                        "osr": 1,
                        "frames_per_gpu": args.frames, "data_symbols_per_frame": args.data_symbols,
                        "parallelism": f"frames sharded x{world}, no collective (gloo timing only)",
