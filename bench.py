@@ -466,10 +466,16 @@ def run_channels(frames, data_syms, steps, warmup, dist, device, rank, chunk_byt
     per_chunk = max(1, int(chunk_bytes // (L * 8)))
     chunks = [(c0, min(per_chunk, frames - c0)) for c0 in range(0, frames, per_chunk)]
     outs = [None] * len(chunks)
+    # the chunks round-robin over STREAMS HIP streams (a workspace each): one chunk's estimate
+    # stages beside another's symbol pass, as bench.py's steps
+    S = max(1, STREAMS)
+    main_stream = torch.cuda.current_stream(device)
+    sts = [main_stream] if S == 1 else [torch.cuda.Stream(device) for _ in range(S)]
 
     def step():
         for i, (c0, n) in enumerate(chunks):
-            outs[i] = plan.run(iq[c0:c0 + n], outs[i])
+            with torch.cuda.stream(sts[i % S]):
+                outs[i] = plan.run(iq[c0:c0 + n], outs[i])
 
     for _ in range(warmup):
         step()
@@ -477,8 +483,14 @@ def run_channels(frames, data_syms, steps, warmup, dist, device, rank, chunk_byt
     barrier(dist)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
+    for st in sts:
+        if st is not main_stream:
+            st.wait_stream(main_stream)
     for _ in range(steps):
         step()
+    for st in sts:
+        if st is not main_stream:
+            main_stream.wait_stream(st)
     torch.cuda.synchronize(device)
     barrier(dist)
     wall = time.perf_counter() - t0
@@ -495,7 +507,7 @@ def run_channels(frames, data_syms, steps, warmup, dist, device, rank, chunk_byt
         pbad += pr["frames_mismatched"]
     del xplan, iq, tx
     return {"frames_per_gpu": frames, "data_symbols_per_frame": data_syms, "iq_gb_per_gpu": frames * L * 8 / 1e9,
-            "chunks": len(chunks), "ms_per_step": wall * 1e3 / steps,
+            "chunks": len(chunks), "streams": S, "ms_per_step": wall * 1e3 / steps,
             "ms_per_step_max_rank": wall_max * 1e3 / steps,
             "value_all_ranks_msym_s": units / wall_max / 1e6,
             "symbols_ok_all_frames": bad == 0, "symbol_mismatches": bad,
