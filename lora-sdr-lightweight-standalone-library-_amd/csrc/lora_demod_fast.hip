@@ -544,6 +544,29 @@ __device__ __forceinline__ void spec_factors(float rate, int l, v2f* F) {
   for (int q = QS; q + 1 < P; q += 2) pk_cmul_chain2(F[q - 1], wd, F[q], F[q + 1]);
   if constexpr (QS < P && ((P - QS) % 2) == 1) F[P - 1] = pk_cmul(F[P - 2], wd);
 }
+// The SF7 pair-load symbol pass's factors (k_spec_demod PL): F[h + 2 m] = e^{i rate (r_h + 16 m)}
+// for the lane's two residues r_h: e^{i rate r_h} and w = e^{i rate 16} from one hardware
+// sin/cos pair each (rate 16 is exact), then 7 complex-product steps per residue (the form
+// of spec_factors' steps).  Error per factor (certify_list's e_spec): the arguments fl(rate r_h)
+// and their products by 1/2pi (3 u rmax 15), w's product (2 u rmax 16) times up to 7 steps -
+// 33.6 u rmax T at T = 8, inside the bound's 36 u rmax T; up to 8 sin/cos and fract errors
+// and 7 product roundings, inside its 16 and 15.
+__device__ __forceinline__ void spec_factors_pl(float rate, const int* r, v2f* F) {
+  constexpr float INV_2PI = 0.159154943091895335768883763372514362f;
+  const float revw = __builtin_amdgcn_fractf((rate * 16.0f) * INV_2PI);
+  const float cw = __builtin_amdgcn_cosf(revw), sw = __builtin_amdgcn_sinf(revw);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float rev0 = __builtin_amdgcn_fractf((rate * (float)r[h]) * INV_2PI);
+    F[h] = v2f{__builtin_amdgcn_cosf(rev0), __builtin_amdgcn_sinf(rev0)};
+  }
+  const v2f wr = {cw, cw}, wi = {-sw, sw};
+#pragma unroll
+  for (int m = 1; m < 8; ++m)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) F[h + 2 * m] = __builtin_elementwise_fma(F[h + 2 * m - 2].yx, wi, F[h + 2 * m - 2] * wr);
+}
+
 // the window's samples times the factors (and the Hann window, LoRaDemod.cpp:158-160), in
 // pass-1 leaf order
 // FOLD: only the leading input of each of pass 1's first-stage butterflies (position p with
@@ -1328,7 +1351,171 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
   // loaded with the table pairs ahead of the prefetch, pass A's are in LDS - so no wait on
   // the current block's operands also waits for the next block's samples (vmcnt retires in
   // order).
-  constexpr bool PF = WL && G::NPASS == 2 && !OSRN;
+  // PL (SF7 unwindowed, round 6): the PF loop with 16-byte sample loads.  A load instruction
+  // reads one whole 128-byte line per symbol (lane l: samples A + 2 l + 16 j and the next,
+  // j < 8) instead of half a line per 8-byte load (lane l: A + l + 8 q, q < 16): half the load
+  // instructions and whole-line requests (an ablation with these loads and unchanged
+  // arithmetic ran the pass 15 % faster).  The transform is the same radix-8 x radix-16 DIT;
+  // only which residues (point index mod 16) a lane holds changes: the two residues r_h =
+  // (2 l + h - d) mod 16 of its elements h (d = the window's offset in its line), instead of
+  // role lr's lr and lr + 8.  Its pass-1 groups are those residues' 8-point transforms, written
+  // back to their positions (rev[r] >> 3 = 4 (r & 3) + (r >> 2) at N = 128); pass A reads by
+  // the lane's own index.  A late element (2 l + h < d) is point m of its residue from load
+  // m + 1 (the 9th: the next window's first line, from the next lane group when contiguous).
+  // Rotation factors e^{i rate (r_h + 16 m)} (spec_factors_pl); the certification's bound
+  // covers them (certify_list: 36 u rmax T).
+#ifndef LORA_SPEC_PAIRLD
+#define LORA_SPEC_PAIRLD 1
+#endif
+  constexpr bool PL = LORA_SPEC_PAIRLD && SF == 7 && !HANN && WL && G::NPASS == 2 && !OSRN;
+  if constexpr (PL) {
+    static_assert(T == 8 && P == 16 && G::G1 == 2 && G::R1 == 8 && G::LOGR1 == 3 && FOLD, "SF7 geometry");
+    constexpr int DL = 16;  // samples per 128-byte line
+    const int tid0 = threadIdx.x;
+    const int g = tid0 / T;
+    const int l = tid0 % T;
+    const int gi = g % SPB;
+    const __attribute__((address_space(4))) FrameParams* fps =
+        (const __attribute__((address_space(4))) FrameParams*)a.fp_spec;
+    struct Blk {
+      int64_t f;
+      int s, d, cg;
+      bool valid, mis, nbr;
+      float rate;
+      int toff;
+    };
+    float4 nx[P / 2 + 1];  // loads j < 8, and the 9th (late elements)
+    auto issue = [&](int64_t bb, Blk& B) {
+      B.f = bb / bpf;
+      const int jl = (int)(bb - B.f * bpf) * SPB + gi;
+      B.valid = jl < per;
+      B.s = S0 + (B.valid ? jl : per - 1);
+      B.rate = RAWM ? 0.0f : fps[B.f].rate;  // scalar loads (constant address space, uniform frame)
+      B.toff = RAWM ? 0 : fps[B.f].t_off;
+      int64_t base;
+      sym_base(B.s, N, a.frame_len, B.toff, base, B.cg);
+      if constexpr (API) B.cg = 0;
+      B.d = (int)(base & (DL - 1));
+      B.mis = __builtin_amdgcn_readfirstlane(__ballot(B.d != 0) != 0);
+      const __amdgpu_buffer_rsrc_t rx =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + B.f * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
+      const int vo = (int)(base - B.d) * 8 + 16 * l;
+#pragma unroll
+      for (int j = 0; j < P / 2; ++j)
+        nx[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, j * DL * 8, 2 /* nt */));
+      B.nbr = false;
+      if (B.mis) {
+        // the late elements' 9th line is the next window's first: when that window is the next
+        // group's (the frame's next symbol, contiguous), taken from it by a lane permute where
+        // the block is consumed; else each late element's own 8-byte load (the line's other
+        // half may lie past the window, past the batch)
+        int64_t bnext;
+        int cgn;
+        sym_base(B.s + 1, N, a.frame_len, B.toff, bnext, cgn);
+        B.nbr = gi < SPB - 1 && jl + 1 < per && bnext == base + N;
+        if (!B.nbr) {
+          if (2 * l < B.d) {
+            const v2f e0 = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, (P / 2) * DL * 8, 2));
+            nx[P / 2].x = e0.x;
+            nx[P / 2].y = e0.y;
+          }
+          if (2 * l + 1 < B.d) {
+            const v2f e1 = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo + 8, (P / 2) * DL * 8, 2));
+            nx[P / 2].z = e1.x;
+            nx[P / 2].w = e1.y;
+          }
+        }
+      }
+    };
+    int64_t b = grp0 * BPG + wave;
+    Blk nb{};
+    if (b < dblocks) issue(b, nb);
+    for (; b < dblocks; b += gstride * BPG, grp0 += gstride) {
+      const Blk B = nb;
+      float4(&ld)[P / 2 + 1] = nx;  // this block's samples, consumed in place
+      const int d = B.d;
+      // the residues of the lane's two elements
+      int r[2];
+      bool late[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int x = 2 * l + h - d;
+        late[h] = x < 0;
+        r[h] = x & (DL - 1);
+      }
+      // the table values of point (h, m) = window point r_h + 16 m (the staged doubled table,
+      // any table phase)
+      cf dv[MODE == 0 ? P : 1];
+      if constexpr (MODE == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const cf* dq = dtab + B.cg + r[h];
+#pragma unroll
+          for (int m = 0; m < P / 2; ++m) dv[h + 2 * m] = dq[DL * m];
+        }
+      }
+      cf in[P];
+      if (B.mis) {
+        // the next group's first line (lane + T), before any lane moves its elements
+        const int src = ((int)__lane_id() + T) & 63;
+        const float4 n0 = {__shfl(ld[0].x, src, 64), __shfl(ld[0].y, src, 64), __shfl(ld[0].z, src, 64),
+                           __shfl(ld[0].w, src, 64)};
+        if (B.nbr) ld[P / 2] = n0;
+#pragma unroll
+        for (int m = 0; m < P / 2; ++m) {
+          in[2 * m] = late[0] ? cf{ld[m + 1].x, ld[m + 1].y} : cf{ld[m].x, ld[m].y};
+          in[2 * m + 1] = late[1] ? cf{ld[m + 1].z, ld[m + 1].w} : cf{ld[m].z, ld[m].w};
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < P / 2; ++m) {
+          in[2 * m] = cf{ld[m].x, ld[m].y};
+          in[2 * m + 1] = cf{ld[m].z, ld[m].w};
+        }
+      }
+      if constexpr (MODE == 0) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) in[q] = pk_cmul_ref(in[q], dv[q]);
+      }
+      float pm = 0.0f;
+#pragma unroll
+      for (int q = 0; q < P; ++q) pm = amax3(pm, in[q]);
+      asm volatile("" : "+v"(pm));
+      cf z[P], wz[P];
+      {
+        v2f F[P];
+        spec_factors_pl(B.rate, r, F);
+        spec_rotate_place<SF, false, FOLD>(in, z, F, a.win, l, wz);
+      }
+      asm volatile("" : "+v"(pm));
+      // the next block's samples, requested once this block's are consumed
+      __builtin_amdgcn_sched_barrier(0);
+      if (b + gstride * BPG < dblocks) issue(b + gstride * BPG, nb);
+      __builtin_amdgcn_sched_barrier(0);
+      // the residues' pass-1 positions: rev[r] >> 3 at N = 128 (kissfft radices 4, 4, 4, 2:
+      // tests/test_capi.py::test_sf7_pair_load_positions checks the identity)
+      int cpre[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) cpre[h] = ((r[h] & 3) << 2) | (r[h] >> 2);
+      const uint64_t lk = fft_key<SF, false, true, (NTW > 0), true, true, NoHook, FOLD>(
+          z, rows + (size_t)g * rowc, l, a, nullptr, twl, cpre, NoHook{}, nullptr, wz);
+      const uint32_t lbest = (uint32_t)lk;
+      uint32_t best = lbest, sec = (uint32_t)(lk >> 32);
+      spec_reduce<SF>(best, sec, pm, tid0, red3);
+      if (B.valid) {
+        constexpr int NG = P / G::RA;
+        constexpr int ML = G::MA_A;
+        const int o = (int)(best & 15u);
+        const uint32_t idx = (uint32_t)(l + T * (o % NG) + ML * (o / NG));
+        const float margin = __builtin_amdgcn_sqrtf(spec_key_value(best)) - __builtin_amdgcn_sqrtf(spec_key_value(sec));
+        if (lbest == best && a.syms) a.syms[B.f * a.sym_stride + (B.s - S0)] = (uint16_t)idx;
+        if (l == 0)
+          reinterpret_cast<uint2*>(a.spec_marg)[B.f * tot + B.s] = make_uint2(__float_as_uint(margin), __float_as_uint(pm));
+      }
+      wave_sync();  // the rows are rewritten by the next round
+    }
+  }
+  constexpr bool PF = WL && G::NPASS == 2 && !OSRN && !PL;
   if constexpr (PF) {
     constexpr int D = T < 8 ? T : 8;
     const int tid0 = threadIdx.x;
@@ -1365,9 +1552,22 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       const __amdgpu_buffer_rsrc_t rx =
           __builtin_amdgcn_make_buffer_rsrc((void*)(a.iq + B.f * a.frame_stride), (short)0, 0x7fffffff, 0x00020000);
       const int vo = (int)(base - B.d + l) * 8;
+#ifdef LORA_ABL_LD16
+      // ablation (results invalid): the window's bytes in 16-byte loads, whole lines per symbol
+      {
+        const int vo2 = (int)(base - B.d) * 8 + 16 * l;
+#pragma unroll
+        for (int pp = 0; pp < P / 2; ++pp) {
+          const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo2, pp * 2 * T * 8, 2));
+          nx[2 * pp] = v2f{v.x, v.y};
+          nx[2 * pp + 1] = v2f{v.z, v.w};
+        }
+      }
+#else
 #pragma unroll
       for (int q = 0; q < P; ++q)
         nx[q] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(rx, vo, q * T * 8, 2 /* nt */));
+#endif
       B.nbr = false;
       if (B.mis) {
         // a late lane's 17th point is the next window's first: when that window is the next
@@ -1690,9 +1890,9 @@ __device__ __forceinline__ void certify_list(const KArgs& a, int64_t f, const Fr
   const double drate = fabs((double)q.rate - (double)qs.rate);
   const double rmax = fmax(fabs((double)q.rate), fabs((double)qs.rate));
   const double tabs = (double)abs(q.t_off);
-  // the speculative rotation factors' error (spec_factors): 33 u rmax T + 16 (fract's
+  // the speculative rotation factors' error (spec_factors, spec_factors_pl): 36 u rmax T + 16 (fract's
   // rounding 2 pi 2^-25 + sqrt2 kHwSinCosErr) + 15 (2 sqrt2 u) + the keys' truncation 2^-20
-  const double e_spec = 33.0 * u * rmax * T + 16.0 * (1.87e-7 + 1.4143 * kHwSinCosErr) + 2.6e-6 + 9.6e-7;
+  const double e_spec = 36.0 * u * rmax * T + 16.0 * (1.87e-7 + 1.4143 * kHwSinCosErr) + 2.6e-6 + 9.6e-7;
   // symbol s certified: its margin d exceeds 4 B (n1 = 2 N x the window's max(|I|,|Q|))
   auto certified = [&](double d, double wmax, int s) {
     const double n1 = 2.0 * N * wmax;
@@ -2081,8 +2281,10 @@ k_est_fast(KArgs a, int64_t frames, int rowc) {
     //    of a negative argument (2^-25 revolutions = 1.87e-7) and v_sin/v_cos_f32
     //    (kHwSinCosErr per component); wd = e^{i r' T} the same without the first term; then
     //    15 packed products by wd, each rounding by <= 2 sqrt2 u: every factor lies within
-    //    e_spec = 33 u rmax T + 16 (1.87e-7 + sqrt2 kHwSinCosErr) + 15 (2 sqrt2 u) of
-    //    e^{i r' i}; the demod ranks bins by keys that truncate |X|^2 by < 16 ulp (spec_key),
+    //    33 u rmax T + 16 (1.87e-7 + sqrt2 kHwSinCosErr) + 15 (2 sqrt2 u) of e^{i r' i} (the
+    //    SF7 pair-load pass's two chains of 8, spec_factors_pl: 33.6 u rmax T, 8 and 7 terms),
+    //    so e_spec = 36 u rmax T + 16 (...) + 15 (...) holds for both; the demod ranks bins by
+    //    keys that truncate |X|^2 by < 16 ulp (spec_key),
     //    moving |X| by < 2^-20 |X|, which e_spec adds;
     //  * the two exact phases r i and r' i differ by at most |r - r'| N;
     //  * every other rounding (the product y * scale, the rotation product, log2 N
@@ -2112,7 +2314,7 @@ __device__ __forceinline__ bool spec_certified(double d, double wmax, int s, dou
   constexpr int T = N >= 16 ? N / 16 : 1;
   const double u = 1.0 / 16777216.0;
   const double E = (8.0 * SF + 42.0) * u;
-  const double e_spec = 33.0 * u * rmax * T + 16.0 * (1.87e-7 + 1.4143 * kHwSinCosErr) + 2.6e-6 + 9.6e-7;
+  const double e_spec = 36.0 * u * rmax * T + 16.0 * (1.87e-7 + 1.4143 * kHwSinCosErr) + 2.6e-6 + 9.6e-7;
   const double n1 = 2.0 * N * wmax;
   const double L = (double)(s + 1) * N + tabs;
   const double e_ref = u * rmax * (L + 2.0 * N);

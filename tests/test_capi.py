@@ -116,3 +116,17 @@ def test_lora_demod_thresh_and_mtu_validation():
         lora_phy_amd.LoRaDemod(7, thresh=-20.0)
     with _pytest.raises(ValueError):
         lora_phy_amd.LoRaDemod(7, mtu=0)
+
+
+def test_sf7_pair_load_positions():
+    """k_spec_demod's SF7 pair-load pass (PL) writes residue r's pass-1 group to position
+    rev[r] >> 3 computed as 4 (r & 3) + (r >> 2): kissfft's leaf order at N = 128 (radices
+    4, 4, 4, 2; tools/lds/lds_sim.leaf_rev, the design aid's replica of the device table)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "lds"))
+    import lds_sim
+
+    rev = lds_sim.leaf_rev(128)
+    assert all(rev[r] >> 3 == ((r & 3) << 2) | (r >> 2) for r in range(16))
