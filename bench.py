@@ -299,7 +299,9 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
         streams_equal = True
     fixed = (plan.spec_recomputed() - fixed0) / steps
     kernels = sorted(plan.last_kernels())
-    stage_ms, out = stage_times(plan, iq, out, steps, device)
+    # (at least 50 launches: with the driver's 20 the per-kernel averages carried the
+    # first launches' ramp, e.g. 0.2114 against 0.1933 ms for the SF7 pass on one box)
+    stage_ms, out = stage_times(plan, iq, out, max(steps, 50), device)
     total_syms = data_syms + 2
     # RAW mode demodulates every symbol of the frame (the sync symbols too)
     out_syms = total_syms if mode == "raw" else data_syms
