@@ -197,9 +197,11 @@ STREAMS_DEFAULT = 2
 STREAMS = STREAMS_DEFAULT
 
 
-def stage_times(plan, iq, out, steps, device):
+def stage_times(plan, iq, out, steps, device, streams=None, outs=None):
     """Per-kernel durations: a second pass of the same steps with HIP events around every
-    launch, recorded on the stream each kernel runs on (outside the timed region)."""
+    launch, recorded on the stream each kernel runs on (outside the timed region).  With
+    `streams`, the steps go round-robin over them as in the timed loop, so each launch runs
+    beside the other batch's kernels as it did there (and as the tracer sees it)."""
     import ctypes as C
 
     import torch
@@ -208,8 +210,19 @@ def stage_times(plan, iq, out, steps, device):
 
     lib = _capi.lib()
     _capi.check(lib.lora_demod_profile_enable(plan._h, steps))
-    for _ in range(steps):
-        out = plan.run(iq, out)
+    if streams and len(streams) > 1:
+        main = torch.cuda.current_stream(device)
+        for st in streams:
+            st.wait_stream(main)
+        for k in range(steps):
+            with torch.cuda.stream(streams[k % len(streams)]):
+                outs[k % len(streams)] = plan.run(iq, outs[k % len(streams)])
+        for st in streams:
+            main.wait_stream(st)
+        out = outs[0]
+    else:
+        for _ in range(steps):
+            out = plan.run(iq, out)
     torch.cuda.synchronize(device)
     stage = (C.c_float * 3)()
     calls = C.c_int()
@@ -301,7 +314,12 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     kernels = sorted(plan.last_kernels())
     # (at least 50 launches: with the driver's 20 the per-kernel averages carried the
     # first launches' ramp, e.g. 0.2114 against 0.1933 ms for the SF7 pass on one box)
+    # the kernels one batch at a time (no other batch's kernels beside them: what the kernel
+    # tracer, which serialises launches, measures) - the roofline's launch time; and with the
+    # steps on the timed loop's streams, where a launch shares the GPU with the other batch's
+    # kernels and its wall time stretches while the step's throughput rises
     stage_ms, out = stage_times(plan, iq, out, max(steps, 50), device)
+    stage_ms_streams = stage_ms if S == 1 else stage_times(plan, iq, out, max(steps, 50), device, sts, outs)[0]
     total_syms = data_syms + 2
     # RAW mode demodulates every symbol of the frame (the sync symbols too)
     out_syms = total_syms if mode == "raw" else data_syms
@@ -341,7 +359,8 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     return {
         "sf": sf, "osr": osr, "mode": mode, "window": window, "precision": precision,
         "frames": frames, "data_symbols": frames * out_syms, "iq_bytes": iq.numel() * 8,
-        "ms_per_step": ms_step, "stage_ms": stage_ms, "symbols_ok": ser == 0.0, "ser_vs_tx": ser,
+        "ms_per_step": ms_step, "stage_ms": stage_ms, "stage_ms_streams": stage_ms_streams,
+        "symbols_ok": ser == 0.0, "ser_vs_tx": ser,
         "streams": S,
         "kernels": kernels, "spec_recomputed_per_step": fixed,
         "msym_s_data": frames * out_syms / (ms_step * 1e-3) / 1e6,
@@ -738,6 +757,13 @@ def roofline(r, probe=None):
     return {"bound": "hbm", "kernel": r["dominant_kernel"],
             "achieved": r["dominant_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": r["dominant_gbs"] / HBM_PEAK_GBS,
+            # achieved / frac: the kernel's HIP-event launch time, one batch at a time (as the
+            # kernel tracer sees it); with_streams: launched as in the timed loop, beside the
+            # other batch's kernels (a longer wall time per launch, a higher step rate)
+            "launch_ms": r["stage_ms"][r["dominant_stage"]],
+            "with_streams": {"launch_ms": r["stage_ms_streams"][r["dominant_stage"]],
+                             "frac": r["dominant_bytes_per_launch"] / (r["stage_ms_streams"][r["dominant_stage"]] * 1e-3)
+                             / 1e9 / HBM_PEAK_GBS},
             "bytes_per_launch": r["dominant_bytes_per_launch"],
             "traffic": pmc_dom,
             "traffic_source": "profiles/pmc_summary.json (rocprofv3 FETCH_SIZE*2+WRITE_SIZE per launch, "
@@ -1001,7 +1027,7 @@ def main():
                        "frames_per_gpu": args.frames, "data_symbols_per_frame": args.data_symbols,
                        "parallelism": f"frames sharded x{world}, no collective (gloo timing only)",
                        "ranks": ranks, "symbols_ok": r7["symbols_ok"], "parity": r7["parity"],
-                       "stage_ms": r7["stage_ms"],
+                       "stage_ms": r7["stage_ms"], "stage_ms_streams": r7["stage_ms_streams"],
                        "kernels": r7["kernels"], "spec_recomputed_per_step": r7["spec_recomputed_per_step"],
                        "msym_s_all_symbols": r7["msym_s_all"] * world,
                        "pipeline_gbs_per_gpu": r7["pipeline_gbs"]},

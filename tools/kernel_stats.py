@@ -55,8 +55,8 @@ def main():
            "Each workload alone (`tools/prof_workload.py`, eager `plan.run` per step).  Resources: code-object "
            "metadata of the built `liblora_mi355x.so` (`tools/kernel_resources.py`); LDS = the metadata's static "
            "bytes + the dynamic bytes the launch requests (`kernel_resources.dynamic_lds`, the launch formulas of "
-           "lora_demod_fast.hip restated; the trace's LDS_Block_Size shows only the static part).  The tracer serialises dispatches; bench.py's "
-           "HIP-event stage times are measured without it.", ""]
+           "lora_demod_fast.hip restated; the trace's LDS_Block_Size shows only the static part).  bench.py's "
+           "HIP-event stage times are measured without the tracer.", ""]
     for tag, what in TAGS.items():
         rows = trace(os.path.join(src, tag))
         if not rows:
@@ -103,11 +103,15 @@ def main():
         out += [f"## {tag}: `python bench.py {'--no-cpu --no-channels --no-fast --no-variants --no-sf12' if key is None else '--sf12-only'}` under rocprofv3 --kernel-trace --stats", "",
                 f"bench.py's HIP-event stage times in the same run (ms per step): estimate stages {stage[1]:.4f}, "
                 f"symbol pass {stage[2]:.4f}; ms_per_step {r['ms_per_step']:.4f} (timed steps: "
-                f"{'one HIP-graph replay' if d.get('config', {}).get('launch') == 'graph' else 'plan.run'} per step; "
-                f"the tracer serialises the kernels)", "",
-                "| kernel | launches | avg us (rocprofv3) |", "|---|---:|---:|"]
+                f"{'one HIP-graph replay' if d.get('config', {}).get('launch') == 'graph' else 'plan.run'} per step, "
+                f"on {d.get('config', {}).get('streams', r.get('streams', 1))} stream(s)).  The stage times "
+                f"are bench.py's one-batch-at-a-time pass; the trace averages every launch of the process - "
+                f"pre-warm, warm-up and timed steps on the streams, where a launch running beside the other "
+                f"batch's kernels takes longer, and the stage passes - so its median is the comparable figure.", "",
+                "| kernel | launches | avg us (rocprofv3) | median us |", "|---|---:|---:|---:|"]
         for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
-            out.append(f"| `{k}` | {len(v)} | {sum(v) / len(v) / 1e3:.2f} |")
+            vs = sorted(v)
+            out.append(f"| `{k}` | {len(v)} | {sum(v) / len(v) / 1e3:.2f} | {vs[len(vs) // 2] / 1e3:.2f} |")
         out.append("")
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     cnt = collections.defaultdict(lambda: collections.defaultdict(int))
