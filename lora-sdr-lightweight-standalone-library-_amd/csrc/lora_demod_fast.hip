@@ -179,6 +179,11 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
   asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+__device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_max3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 
 // In-register DIT stages over x[0..R): positions base + MA*u, group offset k < MA.
 // Radix-2 (optional, only with MA == 1) then radix-4 stages, as kf_work unwinds.
@@ -320,17 +325,25 @@ __device__ __forceinline__ void pass_lds(cf* row, cf* x, int l, const cf* __rest
   }
   if constexpr (LAST && PACK) {
     static_assert(NG * R == 16, "16 bins per lane: a 4-bit ordinal");
+    // keys two at a time: with sec <= best, the runner-up of {best, sec, k1, k2} is
+    // max(sec, med3(best, k1, k2)) and the best max3(best, k1, k2) - the same two keys as
+    // one med3 + max per key (a lane's 16 keys are distinct: their ordinals differ)
     uint32_t best = 0, sec = 0;
+    uint32_t kk[16];
 #pragma unroll
     for (int u = 0; u < R; ++u)
 #pragma unroll
       for (int gg = 0; gg < NG; ++gg) {
         const cf v = x[gg * R + u];
         const float m2 = __builtin_fmaf(v.re, v.re, v.im * v.im);
-        const uint32_t k = spec_key(m2, u * NG + gg);
-        sec = umed3(sec, k, best);  // sec <= best: max(sec, min(k, best))
-        best = best > k ? best : k;
+        kk[u * NG + gg] = spec_key(m2, u * NG + gg);
       }
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      const uint32_t m = umed3(best, kk[i], kk[i + 1]);
+      sec = sec > m ? sec : m;
+      best = umax3(best, kk[i], kk[i + 1]);
+    }
     key = (uint64_t)best | ((uint64_t)sec << 32);
   } else if constexpr (LAST) {
     // The last pass covers all N bins with cc == 0: bin = (l + T*gg) + MA*u.  Scanning
@@ -1385,8 +1398,13 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       int toff;
     };
     float4 nx[P / 2 + 1];  // loads j < 8, and the 9th (late elements)
+    // a block's frame bb / bpf by a reciprocal (exact while dblocks * bpf < 2^32: the
+    // round-up multiplier's error stays below 1 / bpf) instead of a 64-bit division on the
+    // scalar unit per block
+    const bool fdiv = (uint64_t)dblocks * (uint64_t)bpf < (1ull << 32);
+    const uint64_t mq = ((1ull << 32) + (uint64_t)bpf - 1) / (uint64_t)bpf;
     auto issue = [&](int64_t bb, Blk& B) {
-      B.f = bb / bpf;
+      B.f = fdiv ? (bpf == 1 ? bb : (int64_t)(((uint64_t)(uint32_t)bb * mq) >> 32)) : bb / bpf;
       const int jl = (int)(bb - B.f * bpf) * SPB + gi;
       B.valid = jl < per;
       B.s = S0 + (B.valid ? jl : per - 1);
