@@ -486,3 +486,46 @@ def test_raw_mode_through_the_pipeline(O, amd, sf, hann, dechirp):
         assert int(res.sync.to(torch.int32).sum()) == 0 and float(res.cfo.abs().sum()) == 0.0
         if spec and not dechirp:
             assert plan.spec_recomputed() > 0  # the ties at least
+
+
+@pytest.mark.parametrize("dechirp", [True, False])
+@pytest.mark.parametrize("snr_db", [None, 5.0, -10.0])
+def test_sf7_whole_line_pass_every_line_offset(O, amd, dechirp, snr_db):
+    """The SF7 whole-line symbol pass (k_spec_demod PL: lane l holds residues (2l + h - d) mod
+    16 of a window at offset d in its 128-byte line, late elements from the 9th line) at every
+    offset d = 0..15 - a fractional carrier offset per frame from -0.5 to +0.5 bin (estimated
+    time offsets from -64 to +63 samples), sample delays and advances, the windows' last line
+    taken from the next lane group or from the late elements' own loads (a wave's last group,
+    frame ends) - every symbol, sync word and cfo / time_offset bit against the oracle."""
+    sf, N, F, S = 7, 128, 48, 21  # 21 data symbols: blocks of 8 with a partial last one
+    rng = np.random.default_rng(7000 + (0 if snr_db is None else int(snr_db) + 100) + int(dechirp))
+    L = (S + 2) * N
+    iq = np.zeros((F, L), np.complex64)
+    n = np.arange(L)
+    for f in range(F):
+        syms = rng.integers(0, N, S).astype(np.uint16)
+        x = O.lora_modulate(syms, sf, 1, 125000, 1.0, int(rng.integers(0, 256)))
+        d = f % 16 + 16 * (f // 16 % 2)  # offsets 0..31: every d, both halves of a symbol's lead
+        x = np.concatenate([np.zeros(d, np.complex64), x])[:L] if f % 3 else np.concatenate([x[d:], np.zeros(d, np.complex64)])
+        # a fractional carrier offset per frame: the estimate's time offset is -frac N
+        # (LoRaDemod.cpp:127-131), so the frames' windows start at every offset in a line
+        x = (x * np.exp(2j * np.pi * ((f + 0.37) / F - 0.5) * n / N)).astype(np.complex64)
+        if snr_db is not None:
+            sigma = 10.0 ** (-snr_db / 20.0) / np.sqrt(2.0)
+            x = x + sigma * (rng.standard_normal(L) + 1j * rng.standard_normal(L))
+        iq[f] = x.astype(np.complex64)
+    plan = amd.DemodPlan(sf, 1, 125000, "none", dechirp=dechirp)
+    host = iq if dechirp else np.stack([O.dechirp(iq[f], sf) for f in range(F)]).astype(np.complex64)
+    res = plan.run(torch.from_numpy(host).cuda())
+    torch.cuda.synchronize()
+    assert plan.last_kernels() == SPEC
+    syms = res.symbols.cpu().numpy()
+    toffs = set()
+    for f in range(F):
+        osym, osync, ocfo, otoff = O.lora_demodulate(O.dechirp(iq[f], sf), sf, 1, False)
+        np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
+        assert int(res.sync[f]) == osync, f"frame {f} sync"
+        assert bits(res.cfo[f].item()) == bits(ocfo) and bits(res.time_offset[f].item()) == bits(otoff), f"frame {f}"
+        toffs.add(int(round(float(otoff))) % 16)
+    if snr_db is None:
+        assert len(toffs) >= 12, toffs  # the line offsets the frames exercised
