@@ -193,8 +193,14 @@ PREWARM_MS = PREWARM_MS_DEFAULT
 # kernels.  Every step still runs the whole pipeline on its whole batch inside the timed
 # region.  (Round 6, one box, tools/streams_probe.py: SF7 0.2376-0.2406 ms per step on one
 # stream, 0.2205-0.2259 on two, 0.2203-0.2211 on three; SF12 4,000 frames -4 % on two.)
-STREAMS_DEFAULT = 2
+# 0 = by spreading factor: three at SF <= 9 (short symbol passes: a third batch still finds
+# room; SF7 -1 to -4 % against two), two beyond (SF12 on three: +4 %, tools/streams_probe.py)
+STREAMS_DEFAULT = 0
 STREAMS = STREAMS_DEFAULT
+
+
+def streams_for(sf):
+    return STREAMS if STREAMS > 0 else (3 if sf <= 9 else 2)
 
 
 def stage_times(plan, iq, out, steps, device, streams=None, outs=None):
@@ -252,7 +258,7 @@ def run_config(sf, frames, data_syms, steps, warmup, dist, device, snr_db=None, 
     out = None
     # the steps' streams (STREAMS; one for a graph replay): step k on stream k mod S, with
     # outputs of its own
-    S = 1 if LAUNCH == "graph" else max(1, STREAMS if streams is None else streams)
+    S = 1 if LAUNCH == "graph" else max(1, streams_for(sf) if streams is None else streams)
     main_stream = torch.cuda.current_stream(device)
     sts = [main_stream] if S == 1 else [torch.cuda.Stream(device) for _ in range(S)]
     outs = [None] * S
@@ -489,7 +495,7 @@ def run_channels(frames, data_syms, steps, warmup, dist, device, rank, chunk_byt
     outs = [None] * len(chunks)
     # the chunks round-robin over STREAMS HIP streams (a workspace each): one chunk's estimate
     # stages beside another's symbol pass, as bench.py's steps
-    S = max(1, STREAMS)
+    S = max(1, streams_for(sf))
     main_stream = torch.cuda.current_stream(device)
     sts = [main_stream] if S == 1 else [torch.cuda.Stream(device) for _ in range(S)]
 
@@ -813,7 +819,8 @@ def main():
                          "multi-rank launch)")
     ap.add_argument("--streams", type=int, default=STREAMS_DEFAULT,
                     help="HIP streams the consecutive steps go to, round-robin (each its own workspace and "
-                         "outputs: that many batches in flight); 1 = every step on one stream")
+                         "outputs: that many batches in flight); 1 = every step on one stream; 0 (default) = "
+                         "three at SF <= 9, two beyond")
     ap.add_argument("--prewarm-ms", type=float, default=PREWARM_MS_DEFAULT,
                     help="untimed steps of each workload for at least this long before its W warmup steps "
                          "(0: none)")
