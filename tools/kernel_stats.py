@@ -67,9 +67,9 @@ def main():
             a["n"] += 1
             a["ns"].append(e - b)
         out += [f"## {tag}: {what}", "",
-                "| kernel | workgroups | launches | avg us | min us | max us | LDS B (static + dynamic) | VGPR | AGPR | "
-                "scratch B/lane | VGPR spills |",
-                "|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
+                "| kernel | workgroups | launches | avg us | median us | min us | max us | LDS B (static + dynamic) | VGPR | "
+                "AGPR | scratch B/lane | VGPR spills |",
+                "|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
         for (k, wg), a in sorted(agg.items(), key=lambda kv: -sum(kv[1]["ns"])):
             if not k.startswith("k_"):
                 continue
@@ -78,7 +78,8 @@ def main():
             st = r.get("group_segment_fixed_size")
             dy = kernel_resources.dynamic_lds("void " + k)
             lds = f"{st} + {dy}" if st is not None and dy is not None else (f"{st} + ?" if st is not None else "?")
-            out.append(f"| `{k}` | {wg} | {a['n']} | {sum(ns) / len(ns) / 1e3:.2f} | {min(ns) / 1e3:.2f} | "
+            med = sorted(ns)[len(ns) // 2]
+            out.append(f"| `{k}` | {wg} | {a['n']} | {sum(ns) / len(ns) / 1e3:.2f} | {med / 1e3:.2f} | {min(ns) / 1e3:.2f} | "
                        f"{max(ns) / 1e3:.2f} | {lds} | {r.get('vgpr_count', '?')} | {r.get('agpr_count', '?')} | "
                        f"{r.get('private_segment_fixed_size', '?')} | {r.get('vgpr_spill_count', '?')} |")
         pipe = [r for r in rows if r[0].startswith(("k_est", "k_cert", "k_spec"))]
