@@ -75,7 +75,7 @@ pmc)
     for cfg in "7 none 15625 2" "12 none 4000 2"; do
       i=$((i+1))
       echo "== pmc $i sf${cfg%% *} $(date +%T)"
-      timeout -s KILL 150 rocprofv3 --pmc $grp --output-format csv -d $P/pmc$i -o run -- python3 tools/prof_workload.py $cfg > $P/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -3 $P/pmc$i.log; exit 2; }
+      PROF_PREWARM_MS=0 timeout -s KILL 150 rocprofv3 --pmc $grp --output-format csv -d $P/pmc$i -o run -- python3 tools/prof_workload.py $cfg > $P/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -3 $P/pmc$i.log; exit 2; }
     done
   done
   for cfg in "7:7 none 15625 2" "12:12 none 4000 2" "7o2:7 none 15625 2 64 2" "7o4:7 none 15625 2 64 4" \
@@ -84,7 +84,7 @@ pmc)
     for c in FETCH_SIZE WRITE_SIZE; do
       t=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
       echo "== $c $tag $(date +%T)"
-      timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $P/pmc_$t$tag -o run -- python3 tools/prof_workload.py $args > $P/pmc_$t$tag.log 2>&1 || { echo "$c pass failed"; tail -3 $P/pmc_$t$tag.log; exit 2; }
+      PROF_PREWARM_MS=0 timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $P/pmc_$t$tag -o run -- python3 tools/prof_workload.py $args > $P/pmc_$t$tag.log 2>&1 || { echo "$c pass failed"; tail -3 $P/pmc_$t$tag.log; exit 2; }
     done
   done
   exit 0 ;;
