@@ -529,3 +529,32 @@ def test_sf7_whole_line_pass_every_line_offset(O, amd, dechirp, snr_db):
         toffs.add(int(round(float(otoff))) % 16)
     if snr_db is None:
         assert len(toffs) >= 12, toffs  # the line offsets the frames exercised
+
+
+@pytest.mark.parametrize("osr", [1, 2])
+def test_frames_at_unaligned_addresses(O, amd, osr):
+    """Frames that start 8 bytes off a 16-byte boundary - an odd row stride and an odd first
+    sample (a view into a larger tensor) - through the pipeline's 16-byte sample loads (SF7's
+    whole-line pass, osr 2's point pairs): every output equal to the oracle's."""
+    sf, N, F, S = 7, 128, 12, 20
+    L = (S + 2) * N * osr
+    rng = np.random.default_rng(4040 + osr)
+    big = np.zeros((F, L + 3), np.complex64)  # row stride L + 3: odd
+    for f in range(F):
+        syms = rng.integers(0, N, S).astype(np.uint16)
+        x = O.lora_modulate(syms, sf, osr, 125000, 1.0, 0x34)
+        x = x * np.exp(2j * np.pi * ((f + 0.5) / F - 0.5) * np.arange(L) / (N * osr))
+        x = x + 0.2 * (rng.standard_normal(L) + 1j * rng.standard_normal(L))
+        big[f, 1:1 + L] = x.astype(np.complex64)
+    t = torch.from_numpy(big).cuda()[:, 1:1 + L]  # first sample 8 bytes past the row start
+    assert t.stride(0) % 2 == 1 and (t.data_ptr() % 16) == 8
+    plan = amd.DemodPlan(sf, osr, 125000, "none", dechirp=True)
+    res = plan.run(t)
+    torch.cuda.synchronize()
+    assert "spec" in plan.last_kernels()
+    syms = res.symbols.cpu().numpy()
+    for f in range(F):
+        osym, osync, ocfo, otoff = O.lora_demodulate(O.dechirp(big[f, 1:1 + L], sf, osr), sf, osr, False)
+        np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
+        assert int(res.sync[f]) == osync
+        assert bits(res.cfo[f].item()) == bits(ocfo) and bits(res.time_offset[f].item()) == bits(otoff)
