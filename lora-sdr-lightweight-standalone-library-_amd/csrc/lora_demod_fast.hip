@@ -1380,6 +1380,9 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
 #ifndef LORA_SPEC_PAIRLD
 #define LORA_SPEC_PAIRLD 1
 #endif
+#ifndef LORA_SPEC_EARLY
+#define LORA_SPEC_EARLY 1
+#endif
   constexpr bool PL = LORA_SPEC_PAIRLD && SF == 7 && !HANN && WL && G::NPASS == 2 && !OSRN;
   if constexpr (PL) {
     static_assert(T == 8 && P == 16 && G::G1 == 2 && G::R1 == 8 && G::LOGR1 == 3 && FOLD, "SF7 geometry");
@@ -1491,6 +1494,15 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
           in[2 * m + 1] = cf{ld[m].z, ld[m].w};
         }
       }
+      // the next block's samples, requested once this block's are in registers of their own:
+      // before the table products with the fused dechirp (MODE 0: SF7 pass -0.8 %), after
+      // the rotation otherwise (the RAW pass gained nothing there: +0.6 %)
+      constexpr bool EARLY = LORA_SPEC_EARLY && MODE == 0;
+      if constexpr (EARLY) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (b + gstride * BPG < dblocks) issue(b + gstride * BPG, nb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if constexpr (MODE == 0) {
 #pragma unroll
         for (int q = 0; q < P; ++q) in[q] = pk_cmul_ref(in[q], dv[q]);
@@ -1506,10 +1518,11 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
         spec_rotate_place<SF, false, FOLD>(in, z, F, a.win, l, wz);
       }
       asm volatile("" : "+v"(pm));
-      // the next block's samples, requested once this block's are consumed
-      __builtin_amdgcn_sched_barrier(0);
-      if (b + gstride * BPG < dblocks) issue(b + gstride * BPG, nb);
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!EARLY) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (b + gstride * BPG < dblocks) issue(b + gstride * BPG, nb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       // the residues' pass-1 positions: rev[r] >> 3 at N = 128 (kissfft radices 4, 4, 4, 2:
       // tests/test_capi.py::test_sf7_pair_load_positions checks the identity)
       int cpre[2];
