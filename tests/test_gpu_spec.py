@@ -531,11 +531,12 @@ def test_sf7_whole_line_pass_every_line_offset(O, amd, dechirp, snr_db):
         assert len(toffs) >= 12, toffs  # the line offsets the frames exercised
 
 
-@pytest.mark.parametrize("osr", [1, 2])
-def test_frames_at_unaligned_addresses(O, amd, osr):
+@pytest.mark.parametrize("osr,window", [(1, "none"), (2, "none"), (4, "none"), (1, "hann")])
+def test_frames_at_unaligned_addresses(O, amd, osr, window):
     """Frames that start 8 bytes off a 16-byte boundary - an odd row stride and an odd first
     sample (a view into a larger tensor) - through the pipeline's 16-byte sample loads (SF7's
-    whole-line pass, osr 2's point pairs): every output equal to the oracle's."""
+    whole-line pass, osr 2's point pairs, osr 4's line pairs; Hann takes the 8-byte loop):
+    every output equal to the oracle's."""
     sf, N, F, S = 7, 128, 12, 20
     L = (S + 2) * N * osr
     rng = np.random.default_rng(4040 + osr)
@@ -548,13 +549,13 @@ def test_frames_at_unaligned_addresses(O, amd, osr):
         big[f, 1:1 + L] = x.astype(np.complex64)
     t = torch.from_numpy(big).cuda()[:, 1:1 + L]  # first sample 8 bytes past the row start
     assert t.stride(0) % 2 == 1 and (t.data_ptr() % 16) == 8
-    plan = amd.DemodPlan(sf, osr, 125000, "none", dechirp=True)
+    plan = amd.DemodPlan(sf, osr, 125000, window, dechirp=True)
     res = plan.run(t)
     torch.cuda.synchronize()
     assert "spec" in plan.last_kernels()
     syms = res.symbols.cpu().numpy()
     for f in range(F):
-        osym, osync, ocfo, otoff = O.lora_demodulate(O.dechirp(big[f, 1:1 + L], sf, osr), sf, osr, False)
+        osym, osync, ocfo, otoff = O.lora_demodulate(O.dechirp(big[f, 1:1 + L], sf, osr), sf, osr, window == "hann")
         np.testing.assert_array_equal(syms[f], osym, err_msg=f"frame {f}")
         assert int(res.sync[f]) == osync
         assert bits(res.cfo[f].item()) == bits(ocfo) and bits(res.time_offset[f].item()) == bits(otoff)
