@@ -1380,6 +1380,9 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
 #ifndef LORA_SPEC_PAIRLD
 #define LORA_SPEC_PAIRLD 1
 #endif
+#ifndef LORA_PL_CPOL
+#define LORA_PL_CPOL 2  // nt
+#endif
 #ifndef LORA_SPEC_EARLY
 #define LORA_SPEC_EARLY 1
 #endif
@@ -1423,7 +1426,7 @@ k_spec_demod(KArgs a, int64_t frames, int rowc, int64_t gstride) {
       const int vo = (int)(base - B.d) * 8 + 16 * l;
 #pragma unroll
       for (int j = 0; j < P / 2; ++j)
-        nx[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, j * DL * 8, 2 /* nt */));
+        nx[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, j * DL * 8, LORA_PL_CPOL));
       B.nbr = false;
       if (B.mis) {
         // the late elements' 9th line is the next window's first: when that window is the next
