@@ -27,6 +27,8 @@ WORK = {
     "api12": dict(sf=12, frames=4000, mode="api"),
     "hann": dict(sf=7, frames=15625, window="hann"),
     "sf12": dict(sf=12, frames=15625),
+    "sf8": dict(sf=8, frames=15625),
+    "sf9": dict(sf=9, frames=15625),
     "sf12n": dict(sf=12, frames=4000, snr_db=-10.0),
 }
 
